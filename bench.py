@@ -1,0 +1,207 @@
+"""Headline benchmark: frames/s of the full per-frame tracking step at 4096 particles, ViT-B/16 @ 224,
+bf16 (BASELINE.json metric / configs[1]); 1/2/4/8 MI355X by sharding the same 4096 particles (strong
+scaling: the metric is quoted at a fixed particle count).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one frame: predict -> crop + ViT-B/16 forward (HIP graph replay) -> weights -> estimate ->
+resample (+ RCCL all-gathers when N > 1). Frames (synthetic u8 224x224, moving textured target) are
+resident in HBM before the timed region. Rank 0 prints ONE JSON line. Extra fields:
+  roofline      the dominant kernel (the FC1 GEMM by default: the largest FLOP share) timed by HIP events on
+                its own stream in an eager pass after the timed region: achieved TFLOP/s vs the 2.5 PF dense
+                bf16 MFMA peak (MI355X_MICROARCH.md). traffic = null (PMC pass: profiles/).
+  frame_mfma_frac  whole-frame algorithmic FLOPs (35.126 GFLOP/crop) x fps / peak.
+  kernels       per-kernel-type HIP-event averages from the same eager pass.
+  cpu_baseline  the CPU oracle (torch fp32 ViT + C particle-filter ops, "port": the reference has no
+                runnable code) timed on this host's cores on a bounded crop sample, extrapolated to one
+                4096-particle frame (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec @ 4096 particles, ViT-B/16 224px; 1/2/4/8 MI355X scaling"
+PEAK_BF16_TFLOPS = 2500.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--particles", type=int, default=4096, help="global particle count")
+    ap.add_argument("--arch", default="vit_base_patch16_224")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--kernel-frames", type=int, default=2, help="eager frames timed per kernel (roofline)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (s); 0 = skip")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity cores)")
+    return ap.parse_args()
+
+
+def cpu_baseline(arch_name: str, P: int, budget_s: float, threads: int):
+    """Oracle CPU path on a bounded sample: crops through the fp32 torch ViT + the C PF ops at P."""
+    import numpy as np
+    import torch
+
+    from oracle import pf as opf
+    from oracle import vit as ovit
+    from vitparticlefiltertracker_amd.config import ARCHS
+    from vitparticlefiltertracker_amd.frames import synthetic_clip
+    from vitparticlefiltertracker_amd.weights import make_vit_weights
+
+    arch = ARCHS[arch_name]
+    torch.set_num_threads(threads)
+    w = make_vit_weights(arch, seed=0)
+    frame = synthetic_clip(2)[1]
+    rng = np.random.default_rng(0)
+    batch = 8
+    part = np.empty((3, batch), np.float32)
+    part[0], part[1], part[2] = rng.uniform(90, 130, batch), rng.uniform(90, 130, batch), rng.uniform(0.8, 1.2, batch)
+    # warm-up
+    patches = opf.crop_patches(frame, part, (64.0, 64.0), arch.img_size, arch.patch, arch.patch_kp, (0.5,) * 3, (0.5,) * 3)
+    ovit.features_from_patches(torch.from_numpy(patches), w, arch)
+    crops, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        patches = opf.crop_patches(frame, part, (64.0, 64.0), arch.img_size, arch.patch, arch.patch_kp, (0.5,) * 3,
+                                   (0.5,) * 3)
+        ovit.features_from_patches(torch.from_numpy(patches), w, arch)
+        crops += batch
+    t_vit = (time.perf_counter() - t0) / crops
+    # particle-filter ops at the full P (predict, estimate, resample)
+    pp = np.empty((3, P), np.float32)
+    pp[0], pp[1], pp[2] = 112.0, 112.0, 1.0
+    Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
+    t1 = time.perf_counter()
+    opf.predict(pp, 0, 1234, 1, (4.0, 4.0, 0.02), 224, 224, (0.5, 2.0))
+    opf.estimate(Q, pp)
+    opf.resample(Q, 12345)
+    t_pf = time.perf_counter() - t1
+    s_per_frame = t_vit * P + t_pf
+    return {"value": 1.0 / s_per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{crops} crops of {arch_name} fp32 (torch CPU oracle, batch {batch}) in "
+                      f"{t_vit * crops:.1f} s + PF ops at P={P}; extrapolated to one {P}-particle frame "
+                      f"({s_per_frame:.1f} s/frame)"}
+
+
+def main() -> int:
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    if args.particles % world:
+        raise SystemExit("--particles must be divisible by the number of ranks")
+
+    from vitparticlefiltertracker_amd import Tracker, load_config
+    from vitparticlefiltertracker_amd.config import ARCHS
+    from vitparticlefiltertracker_amd.frames import synthetic_clip
+    from vitparticlefiltertracker_amd.vit import KernelTimer
+
+    cfg = load_config({"model": {"arch": args.arch, "dtype": args.dtype}, "particles": {"num": args.particles}})
+    arch = ARCHS[args.arch]
+    n_frames = 1 + args.warmup + args.steps + args.kernel_frames
+    clip = synthetic_clip(n_frames)
+    frames = [torch.from_numpy(f).to(dev) for f in clip]          # resident in HBM before timing
+    tr = Tracker(cfg, device=dev, rank=rank, world_size=world, use_graph=not args.no_graph)
+    tr.init(frames[0], cfg["input"]["bbox0"])
+    for k in range(args.warmup):
+        tr.track(frames[1 + k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        tr.track(frames[1 + args.warmup + k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    fps = args.steps / elapsed
+
+    # per-kernel HIP-event timing in eager mode on the same buffers / stream (after the timed region)
+    timer = KernelTimer()
+    tr.engine.timer = timer
+    use_graph = tr.use_graph
+    tr.use_graph = False
+    base = 1 + args.warmup + args.steps
+    for k in range(args.kernel_frames):
+        tr.track(frames[base + k])
+    tr.use_graph = use_graph
+    tr.engine.timer = None
+    ks = timer.summary()
+    n_loc = args.particles // world
+    M = n_loc * arch.tokens
+    D, F = arch.dim, arch.mlp
+    flops = {"gemm_fc1": 2.0 * M * D * F, "gemm_fc2": 2.0 * M * F * D, "gemm_qkv": 2.0 * M * D * 3 * D,
+             "gemm_proj": 2.0 * M * D * D, "gemm_patch": 2.0 * n_loc * arch.n_patches * arch.patch_k * D,
+             "attention": 2.0 * 2.0 * n_loc * arch.heads * arch.tokens ** 2 * arch.head_dim}
+    for name, v in ks.items():
+        if name in flops:
+            v["tflops"] = flops[name] / (v["avg_ms"] * 1e-3) / 1e12
+    dom = max((n for n in flops if n.startswith("gemm") and n in ks), key=lambda n: ks[n]["total_ms"])
+    ach = ks[dom]["tflops"]
+    gflop_frame = arch.gflop_per_crop() * args.particles
+    line = {
+        "metric": METRIC,
+        "value": round(fps, 4),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16" if args.dtype == "bf16" else "f32",
+        "data": "synthetic: u8 224x224 frames (uniform-noise background, moving 64x64 textured target), "
+                "seeded random-init ViT weights (no pretrained checkpoint offline)",
+        "config": {"workload": f"{args.particles} particles, {args.arch} {args.dtype}, full tracking step per frame",
+                   "particles": args.particles, "particles_per_gpu": n_loc, "arch": args.arch,
+                   "hip_graph": not args.no_graph, "parallelism": f"particle-shard x{world}"},
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "avg_launch_ms": round(ks[dom]["avg_ms"], 4),
+                     "flop_per_launch": flops[dom]},
+        "frame_mfma_frac": round(gflop_frame * 1e9 * fps / (PEAK_BF16_TFLOPS * 1e12 * world), 4),
+        "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                    for k, v in ks.items()},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        try:
+            line["cpu_baseline"] = cpu_baseline(args.arch, args.particles, args.cpu_seconds, threads)
+        except Exception as e:  # report, never fake
+            line["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

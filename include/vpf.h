@@ -1,0 +1,121 @@
+/*
+ * libvpf — C-ABI of the MI355X (gfx950) tracking hot path.
+ *
+ * The reference (tugitbartlomiej/ViTParticleFilterTracker) is a README with no code: its ViT feature
+ * extractor and particle filter are named at /root/reference/README.md:7-8 and driven per frame by
+ * main.py (README.md:37, 42). It has no FFI; the interface each entry point replaces is therefore the
+ * SPEC.md / SURVEY.md §8a row it implements (H1..H14), and the Python binding that a maintainer of the
+ * reference would add is `vitparticlefiltertracker_amd/_lib.py` (INTEGRATION.md shows it).
+ *
+ * Conventions:
+ *   - Every pointer is DEVICE memory unless the parameter name ends in `_host`.
+ *   - The caller allocates every buffer, including workspaces; the library never allocates or frees.
+ *   - Every call only enqueues work on `stream` (a hipStream_t) and never synchronises: re-entrant,
+ *     stream-ordered, asynchronous, graph-capturable.
+ *   - Return value: 0 on success, otherwise a hipError_t code, or VPF_ERR_ARG (-1) for an argument that
+ *     violates the documented shape contract (checked on the host before any launch).
+ *   - bf16 tensors are passed as uint16_t (bit pattern of bfloat16).
+ *   - Particles are structure-of-arrays float[3][ld] (rows x, y, scale), `ld` >= n.
+ */
+#ifndef VPF_H
+#define VPF_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VPF_ERR_ARG (-1)
+
+/* GEMM epilogues (vpf_gemm_bf16 / vpf_gemm_f32) */
+#define VPF_EPI_BIAS 0          /* C = A W^T + bias                                              */
+#define VPF_EPI_BIAS_GELU 1     /* C = gelu_erf(A W^T + bias)                                      */
+#define VPF_EPI_BIAS_RESIDUAL 2 /* C = R + (A W^T + bias); R may alias C                          */
+#define VPF_EPI_PATCH 3         /* row m -> token (m/g2)*(g2+1)+1+m%g2; C = A W^T + bias + pos[1+m%g2] */
+
+/* library identity: returns a static string "libvpf <version> gfx950" */
+const char* vpf_version(void);
+
+/* H1 ParticleFilter.predict: SPEC S2, in place on particles[3][ld] (n local particles whose global
+ * indices start at global_begin). */
+int vpf_predict(float* particles, int64_t n, int64_t ld, int64_t global_begin, uint64_t seed,
+                uint32_t frame, float sig_x, float sig_y, float sig_s, float width, float height,
+                float smin, float smax, void* stream);
+
+/* H2+H3 (A operand of the patch embed): bilinear crop + normalise + im2col, SPEC S3.
+ * frame: uint8[H][W][3]; out: [n * (S/patch)^2][Kp] bf16 (vpf_crop_patches_bf16) or fp32 (_f32).
+ * norm_ab_host: 6 floats {a0,a1,a2,b0,b1,b2} (SPEC S3). Requires Kp % 8 == 0, Kp >= 3*patch^2. */
+int vpf_crop_patches_bf16(const uint8_t* frame, int H, int W, const float* particles, int64_t ld,
+                          int64_t n, float w0, float h0, int S, int patch, int Kp,
+                          const float* norm_ab_host, uint16_t* out, void* stream);
+int vpf_crop_patches_f32(const uint8_t* frame, int H, int W, const float* particles, int64_t ld,
+                         int64_t n, float w0, float h0, int S, int patch, int Kp,
+                         const float* norm_ab_host, float* out, void* stream);
+
+/* H3 (CLS row): tokens[p][0][:] = cls + pos[0] for p < n_part; tokens: [n_part][N][D]. */
+int vpf_cls_rows_bf16(uint16_t* tokens, int64_t n_part, int N, int D, const float* cls,
+                      const float* pos, void* stream);
+int vpf_cls_rows_f32(float* tokens, int64_t n_part, int N, int D, const float* cls, const float* pos,
+                     void* stream);
+
+/* H3/H5/H7/H8: C[M][N] = epilogue(A[M][K] * W[N][K]^T). bf16 in/out, fp32 accumulate (MFMA).
+ * bias: fp32[N]; residual: bf16[M][N] (EPI_BIAS_RESIDUAL, may alias C); pos: fp32[g2+1][N] (EPI_PATCH,
+ * with g2 = patch_rows, M % g2 == 0). Requires K % 64 == 0, N % 8 == 0. */
+int vpf_gemm_bf16(const uint16_t* A, const uint16_t* W, const float* bias, const uint16_t* residual,
+                  const float* pos, int patch_rows, uint16_t* C, int64_t M, int64_t N, int64_t K,
+                  int epilogue, void* stream);
+/* fp32 parity mode: same contract with fp32 tensors (exact-f32 MFMA, v_mfma_f32_32x32x2_f32).
+ * Requires K % 32 == 0. */
+int vpf_gemm_f32(const float* A, const float* W, const float* bias, const float* residual,
+                 const float* pos, int patch_rows, float* C, int64_t M, int64_t N, int64_t K,
+                 int epilogue, void* stream);
+
+/* H4: y = LayerNorm(x) per row (fp32 statistics). Row r of x at x + r*x_stride; D % 4 == 0, D <= 1024. */
+int vpf_layernorm_bf16(const uint16_t* x, int64_t rows, int D, int64_t x_stride, const float* gamma,
+                       const float* beta, float eps, uint16_t* y, int64_t y_stride, void* stream);
+int vpf_layernorm_f32(const float* x, int64_t rows, int D, int64_t x_stride, const float* gamma,
+                      const float* beta, float eps, float* y, int64_t y_stride, void* stream);
+
+/* H6: per (particle, head) softmax(q k^T * scale) v. qkv: [B][N][3][H][hd], out: [B][N][H][hd].
+ * hd == 64, N <= 640. */
+int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd,
+                       float scale, void* stream);
+int vpf_attention_f32(const float* qkv, float* out, int64_t B, int N, int H, int hd, float scale,
+                      void* stream);
+
+/* H9+H10: final LayerNorm of each particle's CLS row (tokens + p*N*D), cosine similarity with the
+ * unit template `tmpl`, w = exp(lam (sim - 1)), Q = floor(w 2^bits) (SPEC S5).
+ * feat_out (optional, may be NULL): fp32[n][D] LN'd CLS features. sim_out (optional): fp32[n]. */
+int vpf_cls_weight_bf16(const uint16_t* tokens, int64_t n, int N, int D, const float* gamma,
+                        const float* beta, float eps, const float* tmpl, float lam, int bits,
+                        float* feat_out, float* sim_out, int64_t* Q, void* stream);
+int vpf_cls_weight_f32(const float* tokens, int64_t n, int N, int D, const float* gamma,
+                       const float* beta, float eps, const float* tmpl, float lam, int bits,
+                       float* feat_out, float* sim_out, int64_t* Q, void* stream);
+
+/* H10 alone (ParticleFilter.update with explicit features): feat fp32[n][D] (already LN'd CLS features),
+ * same weight rule as vpf_cls_weight_*. */
+int vpf_cosine_weight_f32(const float* feat, int64_t n, int D, const float* tmpl, float lam, int bits,
+                          float* sim_out, int64_t* Q, void* stream);
+
+/* H11: shard partial sums, SPEC S6. out_T: int64[1] = sum Q; out_sums: fp64[3] = sum Q*{x,y,s}.
+ * Fixed-order tree reduction (deterministic run to run). */
+int vpf_shard_stats(const int64_t* Q, const float* particles, int64_t ld, int64_t n, int64_t* out_T,
+                    double* out_sums, void* stream);
+
+/* H12: systematic resample of the slots [slot_begin, slot_end) whose positions fall in this shard
+ * (SPEC S7). Q: local weights (n_local); offset: sum of the weights of the shards before this one;
+ * total: global sum T; P: global particle count; U: Philox offset word; uniform != 0 treats every
+ * Q_i as 1 (T == 0 fallback; the caller passes offset/total in those units).
+ * Writes anc_out[j - slot_begin] = global ancestor index (local + global_begin) and
+ * states_out[3][out_ld] (x, y, s of the ancestor). cdf_ws: int64[n_local] workspace. */
+int vpf_resample(const int64_t* Q, int64_t n_local, int64_t global_begin, int64_t offset,
+                 int64_t total, int64_t P, uint32_t U, int uniform, int64_t slot_begin,
+                 int64_t slot_end, const float* particles, int64_t ld, int32_t* anc_out,
+                 float* states_out, int64_t out_ld, int64_t* cdf_ws, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VPF_H */

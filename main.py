@@ -1,0 +1,58 @@
+"""`python main.py [--config config.yaml]` — the entry point the reference documents (README.md:34-38):
+read the config, feed frames to the Tracker, print the tracked positions (README.md:42).
+
+Multi-GPU: `torchrun --nproc-per-node G --master-addr 127.0.0.1 main.py` shards the particles over G GPUs.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--config", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "config.yaml"))
+    ap.add_argument("--frames", type=int, default=None, help="override input.frames")
+    ap.add_argument("--out", default=None, help="write positions as JSON here")
+    args = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+    from vitparticlefiltertracker_amd import Tracker, load_config
+    from vitparticlefiltertracker_amd.frames import iter_frames, synthetic_clip
+
+    cfg = load_config(args.config)
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group("nccl")
+    inp = cfg["input"]
+    n = args.frames or int(inp["frames"])
+    if inp["source"] == "synthetic":
+        frames = synthetic_clip(n, inp["height"], inp["width"], tuple(inp["bbox0"]), inp["seed"])
+    else:
+        frames = list(iter_frames(inp["source"]))[:n]
+    tr = Tracker(cfg)
+    tr.init(frames[0], inp["bbox0"])
+    t0 = time.perf_counter()
+    out = []
+    for k, f in enumerate(frames[1:], start=1):
+        x, y, s = tr.track(f)
+        out.append({"frame": k, "x": x, "y": y, "scale": s})
+        if tr.rank == 0:
+            print(f"frame {k:4d}  x={x:8.2f}  y={y:8.2f}  scale={s:6.3f}", flush=True)
+    dt = time.perf_counter() - t0
+    if tr.rank == 0:
+        print(f"{len(out)} frames in {dt:.3f} s ({len(out) / max(dt, 1e-9):.2f} frames/s)", file=sys.stderr)
+        if args.out:
+            with open(args.out, "w") as fh:
+                json.dump(out, fh, indent=1)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,283 @@
+"""GPU (MI355X): every libvpf kernel, called through the product ops / C-ABI, against the oracle (bit-exact
+for integer / byte / fixed-function work) or a torch fp32/fp64 reference of the same op (tolerances in
+each test). Run: python -m pytest tests -m gpu."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+from oracle import pf
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded():
+    from vitparticlefiltertracker_amd import _lib, ops  # noqa: F401
+    L = _lib.lib()
+    assert b"gfx950" in L.vpf_version()
+    assert torch.cuda.is_available()
+
+
+def vpf():
+    return torch.ops.vpf
+
+
+def bf16_bits(x: np.ndarray) -> np.ndarray:
+    """fp32 -> bf16 round-to-nearest-even bit patterns (reference for the bf16 kernels' outputs)."""
+    u = x.astype(np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+# ------------------------------------------------------------------ H1 predict
+@pytest.mark.parametrize("n,begin", [(1, 0), (1000, 0), (4096, 12288), (65536, 0)])
+def test_predict_bit_exact(n, begin):
+    rng = np.random.default_rng(n)
+    p = np.empty((3, n), np.float32)
+    p[0] = rng.uniform(0, 223, n); p[1] = rng.uniform(0, 223, n); p[2] = rng.uniform(0.5, 2.0, n)
+    ref = p.copy()
+    pf.predict(ref, begin, 1234, 7, (4.0, 4.0, 0.02), 224, 224, (0.5, 2.0))
+    d = torch.from_numpy(p).to(DEV)
+    vpf().predict_(d, begin, 1234, 7, [4.0, 4.0, 0.02], 224.0, 224.0, [0.5, 2.0])
+    got = d.cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+# ------------------------------------------------------------------ H2/H3 crop
+@pytest.mark.parametrize("S,patch,H,W", [(224, 16, 224, 224), (336, 14, 240, 320), (224, 16, 1080, 1920)])
+def test_crop_bit_exact(S, patch, H, W):
+    rng = np.random.default_rng(S + H)
+    frame = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    n = 5
+    p = np.empty((3, n), np.float32)
+    p[0] = [W / 2, 0.0, W - 1.0, 13.7, -40.0]
+    p[1] = [H / 2, 5.5, H - 1.0, 101.3, -40.0]
+    p[2] = [1.0, 0.5, 2.0, 1.37, 1.0]
+    kp = (3 * patch * patch + 63) // 64 * 64
+    box = (64.0, 48.0)
+    ref = pf.crop_patches(frame, p, box, S, patch, kp, (0.5, 0.4, 0.3), (0.5, 0.25, 0.2))
+    from vitparticlefiltertracker_amd.vit import norm_affine
+    ab = norm_affine((0.5, 0.4, 0.3), (0.5, 0.25, 0.2))
+    a, b = pf.norm_affine((0.5, 0.4, 0.3), (0.5, 0.25, 0.2))
+    assert np.array_equal(np.array(ab[:3], np.float32), a) and np.array_equal(np.array(ab[3:], np.float32), b)
+    fd, pd = torch.from_numpy(frame).to(DEV), torch.from_numpy(p).to(DEV)
+    g = S // patch
+    out32 = torch.empty(n * g * g, kp, device=DEV, dtype=torch.float32)
+    vpf().crop_patches(fd, pd, list(box), S, patch, ab, out32)
+    assert np.array_equal(out32.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    out16 = torch.empty(n * g * g, kp, device=DEV, dtype=torch.bfloat16)
+    vpf().crop_patches(fd, pd, list(box), S, patch, ab, out16)
+    assert np.array_equal(out16.cpu().view(torch.int16).numpy().view(np.uint16), bf16_bits(ref))
+
+
+# ------------------------------------------------------------------ GEMM
+def _epi_ref(acc, bias, epi, residual=None):
+    y = acc + bias
+    if epi == 1:
+        y = Fn.gelu(y)
+    if epi == 2:
+        y = residual.float() + y.to(torch.bfloat16).float()
+    return y
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 192, 192), (1000, 768, 768), (513, 2304, 768),
+                                   (777, 768, 3072), (64, 520, 128), (4096 * 197 // 64, 3072, 768)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm_bf16(M, N, K, epi):
+    torch.manual_seed(M * 7 + N + K + epi)
+    A = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV) * 0.1
+    R = (torch.randn(M, N, device=DEV)).to(torch.bfloat16) if epi == 2 else None
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    Rin = R.clone() if R is not None else None
+    vpf().gemm(A, W, bias, Rin, None, 0, epi, out)
+    ref = _epi_ref(A.float() @ W.float().t(), bias, epi, R)
+    torch.testing.assert_close(out.float(), ref, rtol=1.6e-2, atol=1e-2)
+    if epi == 2:   # in-place residual (out aliases the residual), as the encoder uses it
+        h = R.clone()
+        vpf().gemm(A, W, bias, h, None, 0, epi, h)
+        assert torch.equal(h, out)
+
+
+def test_gemm_bf16_asymmetric_identity():
+    """A = I with an asymmetric W catches a transposed C write (cdna_hip_programming.md §3)."""
+    M = N = K = 256
+    A = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
+    W = (torch.arange(N * K, device=DEV, dtype=torch.float32).reshape(N, K) % 97 - 48).to(torch.bfloat16)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    vpf().gemm(A, W, torch.zeros(N, device=DEV), None, None, 0, 0, out)
+    assert torch.equal(out, W.t().contiguous())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gemm_patch_epilogue(dtype):
+    torch.manual_seed(5)
+    n, g2, D, K = 3, 196, 192, 768
+    M = n * g2
+    A = (torch.randn(M, K, device=DEV) * 0.5).to(dtype)
+    W = (torch.randn(D, K, device=DEV) * 0.03).to(dtype)
+    bias = torch.randn(D, device=DEV) * 0.1
+    pos = torch.randn(g2 + 1, D, device=DEV) * 0.1
+    out = torch.full((n, g2 + 1, D), 7.0, device=DEV, dtype=dtype)
+    vpf().gemm(A, W, bias, None, pos, g2, 3, out)
+    ref = ((A.double() @ W.double().t()) + bias.double()).reshape(n, g2, D) + pos[1:].double()
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out[:, 1:].double(), ref, **tol)
+    assert torch.all(out[:, 0] == 7.0)       # CLS rows untouched
+    cls = torch.randn(D, device=DEV)
+    vpf().cls_rows_(out, cls, pos)
+    torch.testing.assert_close(out[:, 0].float(), (cls + pos[0]).expand(n, D).to(dtype).float())
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (300, 192, 192), (1000, 768, 768)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm_f32(M, N, K, epi):
+    torch.manual_seed(M + N + K + epi)
+    A = torch.randn(M, K, device=DEV)
+    W = torch.randn(N, K, device=DEV) / K ** 0.5
+    bias = torch.randn(N, device=DEV)
+    R = torch.randn(M, N, device=DEV) if epi == 2 else None
+    out = torch.empty(M, N, device=DEV)
+    vpf().gemm(A, W, bias, R, None, 0, epi, out)
+    acc = A.double() @ W.double().t() + bias.double()
+    ref = Fn.gelu(acc) if epi == 1 else (acc + R.double() if epi == 2 else acc)
+    torch.testing.assert_close(out.double(), ref, rtol=2e-5, atol=2e-5)
+
+
+# ------------------------------------------------------------------ LayerNorm
+@pytest.mark.parametrize("rows,D", [(1, 192), (1000, 768), (333, 1024), (64, 4)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_layernorm(rows, D, dtype):
+    torch.manual_seed(rows + D)
+    x = (torch.randn(rows, D, device=DEV) * 2 + 0.5).to(dtype)
+    g = 1 + 0.1 * torch.randn(D, device=DEV)
+    b = 0.1 * torch.randn(D, device=DEV)
+    y = torch.empty_like(x)
+    vpf().layernorm(x, g, b, 1e-6, y)
+    ref = Fn.layer_norm(x.double(), (D,), g.double(), b.double(), 1e-6)
+    tol = dict(rtol=1e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(y.double(), ref, **tol)
+
+
+# ------------------------------------------------------------------ attention
+@pytest.mark.parametrize("B,N,H", [(3, 197, 12), (2, 577, 16), (5, 1, 3), (4, 64, 2), (2, 100, 1)])
+def test_attention_bf16(B, N, H):
+    torch.manual_seed(B * N + H)
+    D = 64 * H
+    qkv = (torch.randn(B, N, 3 * D, device=DEV) * 1.5).to(torch.bfloat16)
+    out = torch.empty(B, N, D, device=DEV, dtype=torch.bfloat16)
+    vpf().attention(qkv, H, out)
+    q, k, v = qkv.float().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = torch.softmax((q @ k.transpose(-1, -2)) * 0.125, -1) @ v
+    ref = ref.transpose(1, 2).reshape(B, N, D)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 197, 3), (1, 50, 2)])
+def test_attention_f32(B, N, H):
+    torch.manual_seed(N)
+    D = 64 * H
+    qkv = torch.randn(B, N, 3 * D, device=DEV)
+    out = torch.empty(B, N, D, device=DEV)
+    vpf().attention(qkv, H, out)
+    q, k, v = qkv.double().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax((q @ k.transpose(-1, -2)) * 0.125, -1) @ v).transpose(1, 2).reshape(B, N, D)
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------ H9/H10 weights
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_cls_weight(dtype):
+    torch.manual_seed(9)
+    n, N, D = 257, 5, 768
+    tok = torch.randn(n, N, D, device=DEV).to(dtype)
+    g = 1 + 0.1 * torch.randn(D, device=DEV)
+    b = 0.1 * torch.randn(D, device=DEV)
+    t = torch.randn(D, device=DEV)
+    t = t / t.norm()
+    Q = torch.empty(n, device=DEV, dtype=torch.int64)
+    feat = torch.empty(n, D, device=DEV)
+    sim = torch.empty(n, device=DEV)
+    vpf().cls_weight(tok, g, b, 1e-6, t, 20.0, 40, Q, feat, sim)
+    f_ref = Fn.layer_norm(tok[:, 0].double(), (D,), g.double(), b.double(), 1e-6)
+    torch.testing.assert_close(feat.double(), f_ref, rtol=1e-5, atol=1e-5)
+    s_ref = (f_ref @ t.double()) / f_ref.norm(dim=1)
+    torch.testing.assert_close(sim.double(), s_ref, rtol=0, atol=2e-6)
+    # Q is the exact SPEC S5 function of the kernel's own sim (fixed expf, floor at 2^40)
+    q_ref = pf.weights_to_Q(sim.cpu().numpy(), 20.0, 40)
+    assert np.array_equal(Q.cpu().numpy(), q_ref)
+    # explicit-feature path (ParticleFilter.update)
+    Q2 = torch.empty_like(Q)
+    vpf().cosine_weight(feat, t, 20.0, 40, Q2)
+    assert np.array_equal(Q2.cpu().numpy(), q_ref)
+
+
+# ------------------------------------------------------------------ H11/H12
+def test_shard_stats():
+    rng = np.random.default_rng(3)
+    n = 5000
+    Q = rng.integers(0, 1 << 40, n, dtype=np.int64)
+    p = rng.uniform(0, 224, (3, n)).astype(np.float32)
+    T, sums = pf.shard_stats(Q, p)
+    To = torch.empty(1, device=DEV, dtype=torch.int64)
+    So = torch.empty(3, device=DEV, dtype=torch.float64)
+    vpf().shard_stats(torch.from_numpy(Q).to(DEV), torch.from_numpy(p).to(DEV), To, So)
+    assert int(To.item()) == T
+    np.testing.assert_allclose(So.cpu().numpy(), sums, rtol=1e-13)
+
+
+@pytest.mark.parametrize("P", [1, 2, 7, 4096, 65536])
+@pytest.mark.parametrize("mode", ["dense", "sparse", "zero", "onehot"])
+def test_resample_bit_exact(P, mode):
+    rng = np.random.default_rng(P)
+    Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
+    if mode == "sparse":
+        Q[rng.random(P) < 0.9] = 0
+    if mode == "zero":
+        Q[:] = 0
+    if mode == "onehot":
+        Q[:] = 0
+        Q[P // 3] = 12345
+    p = rng.uniform(0, 224, (3, P)).astype(np.float32)
+    U = int(rng.integers(0, 2 ** 32))
+    ref = pf.resample(Q, U)
+    from vitparticlefiltertracker_amd.particle_filter import plan_resample
+    uniform, T, offs, ranges = plan_resample([(int(Q.sum()), 0, 0, 0)], P, P, U)
+    anc = torch.empty(P, device=DEV, dtype=torch.int32)
+    states = torch.empty(3, P, device=DEV)
+    cdf = torch.empty(P, device=DEV, dtype=torch.int64)
+    pd = torch.from_numpy(p).to(DEV)
+    vpf().resample(torch.from_numpy(Q).to(DEV), 0, 0, T, P, U, uniform, 0, P, pd, anc, states, cdf)
+    assert np.array_equal(anc.cpu().numpy(), ref)
+    assert np.array_equal(states.cpu().numpy(), p[:, ref])
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_resample_sharded_equals_global(G):
+    """Per-shard kernel calls with the host plan reproduce the global ancestors (bit-exact, any G)."""
+    from vitparticlefiltertracker_amd.particle_filter import plan_resample
+    rng = np.random.default_rng(G)
+    P = 4096
+    n = P // G
+    Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
+    Q[rng.random(P) < 0.7] = 0
+    p = rng.uniform(0, 224, (3, P)).astype(np.float32)
+    U = int(rng.integers(0, 2 ** 32))
+    ref = pf.resample(Q, U)
+    stats = [(int(Q[r * n:(r + 1) * n].sum()), 0, 0, 0) for r in range(G)]
+    uniform, T, offs, ranges = plan_resample(stats, P, n, U)
+    got = []
+    for r in range(G):
+        a, b = ranges[r]
+        if b == a:
+            continue
+        anc = torch.empty(b - a, device=DEV, dtype=torch.int32)
+        st = torch.empty(3, b - a, device=DEV)
+        cdf = torch.empty(n, device=DEV, dtype=torch.int64)
+        vpf().resample(torch.from_numpy(Q[r * n:(r + 1) * n].copy()).to(DEV), r * n, offs[r], T, P, U, uniform, a, b,
+                       torch.from_numpy(p[:, r * n:(r + 1) * n].copy()).to(DEV), anc, st, cdf)
+        got.append(anc.cpu().numpy())
+    assert np.array_equal(np.concatenate(got), ref)

@@ -1,0 +1,194 @@
+"""CPU: pin the particle-filter oracle (oracle/pf_oracle.c) — Philox KATs, elementary functions,
+predict / crop / resample known-answer tests and properties (SURVEY.md §4 'KAT, PF' and 'Property')."""
+import math
+
+import numpy as np
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from oracle import pf
+
+
+# Random123 published known-answer vectors for philox4x32-10 (kat_vectors)
+PHILOX_KAT = [
+    ((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+    ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+    ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+     (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)),
+]
+
+
+@pytest.mark.parametrize("ctr,key,expect", PHILOX_KAT)
+def test_philox_kat(ctr, key, expect):
+    assert tuple(int(v) for v in pf.philox4x32_10(ctr, key)) == expect
+
+
+def test_fixed_math_accuracy():
+    L = pf.lib()
+    xs = np.linspace(1e-7, 1.0, 20001, dtype=np.float32)
+    err = max(abs(L.orc_logf(float(x)) - math.log(float(x))) for x in xs)
+    assert err < 2e-6
+    for x in np.linspace(-80, 5, 2001, dtype=np.float32):
+        assert abs(L.orc_expf(float(x)) - math.exp(float(x))) <= 2e-7 * math.exp(float(x)) + 1e-45
+    import ctypes
+    c, s = ctypes.c_float(), ctypes.c_float()
+    for u in np.linspace(0, 1, 4001, endpoint=False, dtype=np.float32):
+        L.orc_sincos2pi(float(u), ctypes.byref(c), ctypes.byref(s))
+        assert abs(c.value - math.cos(2 * math.pi * float(u))) < 5e-7
+        assert abs(s.value - math.sin(2 * math.pi * float(u))) < 5e-7
+
+
+def _particles(n, x=100.0, y=100.0, s=1.0):
+    p = np.empty((3, n), np.float32)
+    p[0], p[1], p[2] = x, y, s
+    return p
+
+
+def test_predict_deterministic_and_shard_independent():
+    full = _particles(1000)
+    pf.predict(full, 0, 1234, 3, (4.0, 4.0, 0.02), 224, 224, (0.5, 2.0))
+    again = _particles(1000)
+    pf.predict(again, 0, 1234, 3, (4.0, 4.0, 0.02), 224, 224, (0.5, 2.0))
+    assert np.array_equal(full, again)
+    # the same global indices predicted in two shards give the same bits
+    a, b = _particles(400), _particles(600)
+    pf.predict(a, 0, 1234, 3, (4.0, 4.0, 0.02), 224, 224, (0.5, 2.0))
+    pf.predict(b, 400, 1234, 3, (4.0, 4.0, 0.02), 224, 224, (0.5, 2.0))
+    assert np.array_equal(np.concatenate([a, b], 1), full)
+    # other frame / seed -> different noise
+    c = _particles(1000)
+    pf.predict(c, 0, 1234, 4, (4.0, 4.0, 0.02), 224, 224, (0.5, 2.0))
+    assert not np.array_equal(c, full)
+
+
+def test_predict_noise_statistics():
+    n = 200000
+    p = _particles(n, 1e6, 1e6, 1.0)
+    pf.predict(p, 0, 99, 1, (1.0, 2.0, 0.05), 4e6, 4e6, (1e-3, 1e3))
+    dx, dy = p[0].astype(np.float64) - 1e6, p[1].astype(np.float64) - 1e6
+    ls = np.log(p[2].astype(np.float64))
+    assert abs(dx.mean()) < 0.01 and abs(dx.std() - 1.0) < 0.01
+    assert abs(dy.mean()) < 0.02 and abs(dy.std() - 2.0) < 0.02
+    assert abs(ls.std() - 0.05) < 0.001
+    assert abs(np.corrcoef(dx, dy)[0, 1]) < 0.01
+
+
+def test_predict_clamps():
+    p = _particles(5000, 0.0, 223.0, 1.99)
+    pf.predict(p, 0, 5, 1, (50.0, 50.0, 0.5), 224, 224, (0.5, 2.0))
+    assert p[0].min() >= 0 and p[0].max() <= 223 and p[1].min() >= 0 and p[1].max() <= 223
+    assert p[2].min() >= 0.5 and p[2].max() <= 2.0
+
+
+def test_crop_identity_kat():
+    """box == frame, centred: bilinear samples exact pixel centres -> im2col of the normalised frame."""
+    rng = np.random.default_rng(0)
+    frame = rng.integers(0, 256, (224, 224, 3), dtype=np.uint8)
+    part = np.array([[112.0], [112.0], [1.0]], np.float32)
+    out = pf.crop_patches(frame, part, (224.0, 224.0), 224, 16, 768, (0.5, 0.5, 0.5), (0.5, 0.5, 0.5))
+    a, b = pf.norm_affine((0.5,) * 3, (0.5,) * 3)
+    norm = (frame.astype(np.float64) * a.astype(np.float64) + b.astype(np.float64)).astype(np.float32)  # fmaf
+    img = norm.transpose(2, 0, 1)                                              # CHW
+    ref = img.reshape(3, 14, 16, 14, 16).transpose(1, 3, 0, 2, 4).reshape(196, 768)
+    assert np.array_equal(out, ref)
+
+
+def test_crop_zero_padding_and_kp_pad():
+    frame = np.full((50, 60, 3), 200, np.uint8)
+    part = np.array([[-500.0], [-500.0], [1.0]], np.float32)      # box entirely outside the frame
+    out = pf.crop_patches(frame, part, (32.0, 32.0), 28, 14, 640, (0.5,) * 3, (0.5,) * 3)
+    a, b = pf.norm_affine((0.5,) * 3, (0.5,) * 3)
+    assert out.shape == (4, 640)
+    assert np.all(out[:, :588] == b[0]) and np.all(out[:, 588:] == 0)
+
+
+def _py_resample(Q, U):
+    Q = np.asarray(Q, np.int64)
+    P = len(Q)
+    if Q.sum() == 0:
+        Q = np.ones(P, np.int64)
+    T = int(Q.sum())
+    C = np.cumsum(Q)
+    u = (U * T) >> 32
+    pos = [(j * T + u) // P for j in range(P)]
+    return np.array([int(np.searchsorted(C, p, side="right")) for p in pos], np.int32)
+
+
+@pytest.mark.parametrize("Q,U,expect", [
+    ([1, 1, 1, 1], 0, [0, 1, 2, 3]),
+    ([0, 0, 5, 0], 123456789, [2, 2, 2, 2]),
+    ([3, 1, 0, 4], 2 ** 31, [0, 1, 3, 3]),
+    ([1, 2, 3, 4, 5, 6, 7, 8], 0, [0, 2, 3, 4, 5, 6, 6, 7]),
+    ([1, 2, 3, 4, 5, 6, 7, 8], 2 ** 32 - 1, [2, 3, 4, 5, 6, 6, 7, 7]),
+    ([0, 0, 0, 0, 0], 77, [0, 1, 2, 3, 4]),          # T == 0 -> uniform fallback
+    ([5], 999, [0]),
+    ([0, 7], 5, [1, 1]),
+])
+def test_resample_kat(Q, U, expect):
+    assert pf.resample(np.array(Q, np.int64), U).tolist() == expect
+
+
+def test_resample_uniform_identity_large():
+    P = 1 << 16
+    Q = np.full(P, 1 << 40, np.int64)
+    for U in (0, 1, 2 ** 31, 2 ** 32 - 1):
+        assert np.array_equal(pf.resample(Q, U), np.arange(P, dtype=np.int32))
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.integers(1, 300), st.integers(0, 2 ** 32 - 1), st.integers(0, 2 ** 31), st.booleans())
+def test_resample_properties(P, U, seed, sparse):
+    rng = np.random.default_rng(seed)
+    Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
+    if sparse:
+        Q[rng.random(P) < 0.8] = 0
+    anc = pf.resample(Q, U)
+    assert np.array_equal(anc, _py_resample(Q, U))           # exact 64-bit arithmetic == big-int spec
+    assert np.all(np.diff(anc) >= 0)                          # monotone ancestors
+    if Q.sum() > 0:
+        assert np.all(Q[anc] > 0)                             # never a zero-weight ancestor
+        counts = np.bincount(anc, minlength=P)
+        expect = Q.astype(np.float64) * P / Q.sum()
+        assert np.all(np.abs(counts - expect) < 1.0 + 1e-9)   # systematic: |n_i - P w_i| < 1
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.integers(1, 2 ** 16), st.integers(0, (1 << 56)), st.integers(0, 2 ** 32 - 1))
+def test_position_exact(P, T, U):
+    T = max(T, 1)
+    for j in (0, 1, P // 2, P - 1):
+        assert pf.position(j, T, P, U) == (j * T + ((U * T) >> 32)) // P
+
+
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+def test_resample_shard_invariance(G):
+    """Emulate G shards with the product's host plan (slot ranges from shard totals) + local searches:
+    the ancestors equal the global oracle's for every G (SURVEY.md §8e exactness)."""
+    from vitparticlefiltertracker_amd.particle_filter import plan_resample
+    rng = np.random.default_rng(G)
+    P = 4096
+    Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
+    Q[rng.random(P) < 0.5] = 0
+    U = int(rng.integers(0, 2 ** 32))
+    ref = pf.resample(Q, U)
+    n = P // G
+    stats = [(int(Q[r * n:(r + 1) * n].sum()), 0.0, 0.0, 0.0) for r in range(G)]
+    uniform, T, offsets, ranges = plan_resample(stats, P, n, U)
+    out = []
+    for r in range(G):
+        a, b = ranges[r]
+        C = np.cumsum(Q[r * n:(r + 1) * n])
+        for j in range(a, b):
+            lp = pf.position(j, T, P, U) - offsets[r]
+            out.append(r * n + int(np.searchsorted(C, lp, side="right")))
+    assert np.array_equal(np.array(out, np.int32), ref)
+
+
+def test_estimate_and_weights():
+    p = np.array([[1.0, 2.0, 3.0], [4.0, 5.0, 6.0], [1.0, 1.0, 2.0]], np.float32)
+    assert pf.estimate(np.array([1, 1, 2], np.int64), p) == pytest.approx((9 / 4, 21 / 4, 6 / 4))
+    assert pf.estimate(np.zeros(3, np.int64), p) == pytest.approx((2.0, 5.0, 4 / 3))
+    Q = pf.weights_to_Q(np.array([1.0, 0.0, -1.0], np.float32), 20.0, 40)
+    assert Q[0] == 1 << 40
+    assert Q[1] == int(np.floor(np.float64(np.float32(math.exp(-20.0))) * 2 ** 40)) or abs(Q[1] - math.exp(-20) * 2 ** 40) < 2 ** 40 * 1e-15
+    assert 0 <= Q[2] < 2

@@ -1,0 +1,47 @@
+"""Design aid: LDS bank-conflict counts for the GEMM's LDS images (rules: MI355X_MICROARCH.md §LDS)."""
+G128 = [[0,1,2,3,12,13,14,15,20,21,22,23,24,25,26,27],[4,5,6,7,8,9,10,11,16,17,18,19,28,29,30,31]]
+G128 += [[l+32 for l in g] for g in G128]
+def cycles_read128(addr):          # addr[lane] byte address, 16B per lane, bank=(a/4)%64
+    tot = 0
+    for g in G128:
+        banks = {}
+        for l in g:
+            for d in range(4):
+                b = (addr[l]//4 + d) % 64
+                banks.setdefault(b, set()).add(addr[l]//4 + d)
+        tot += max(len(v) for v in banks.values())
+    return tot   # 4 = conflict-free
+def cycles_write64(addr):          # ds_write_b64: 4 groups of 16 contiguous lanes, bank=(a/4)%32
+    tot = 0
+    for g in range(4):
+        banks = {}
+        for l in range(16*g, 16*g+16):
+            for d in range(2):
+                b = (addr[l]//4 + d) % 32
+                banks.setdefault(b, set()).add(addr[l]//4 + d)
+        tot += max(len(v) for v in banks.values())
+    return tot   # 4 = conflict-free
+swz = lambda r: (r >> 1) & 7
+# main-loop operand read: 16x16x32 fragment, row = base + (lane&15), chunk = 4*ks + (lane>>4)
+worst = 0
+for base in range(0, 256, 16):
+    for ks in range(2):
+        addr = [(base + (l & 15)) * 128 + (((4*ks + (l >> 4)) ^ swz(base + (l & 15))) * 16) for l in range(64)]
+        worst = max(worst, cycles_read128(addr))
+print("operand ds_read_b128 worst cycles (4=free):", worst)
+# glds write image is lane-linear: nothing to check. Epilogue image [m][64 n] bf16, 8B chunk c=n/4 swizzled c^(m&15)
+esw = lambda m: m & 15
+worst = 0
+for ti in range(8):
+    for tj in range(4):
+        addr = [((ti*16 + (l & 15)) * 128) + (((tj*4 + (l >> 4)) ^ esw(ti*16 + (l & 15))) * 8) for l in range(64)]
+        worst = max(worst, cycles_write64(addr))
+print("epilogue ds_write_b64 worst cycles (4=free):", worst)
+worst = 0
+for it in range(16):
+    addr = []
+    for l in range(64):
+        m = it*8 + l//8; c16 = l % 8
+        addr.append(m*128 + ((c16 ^ (esw(m) >> 1)) * 16))
+    worst = max(worst, cycles_read128(addr))
+print("epilogue ds_read_b128 worst cycles (4=free):", worst)

@@ -1,0 +1,125 @@
+"""Configuration surface: the `config.yaml` schema the reference names but does not ship.
+
+The reference's only statement about configuration is "configure the tracking parameters in the
+`config.yaml` file" (/root/reference/README.md:42); the key set below is the build's contract
+ and SPEC.md gives each value its meaning.
+"""
+from __future__ import annotations
+
+import copy
+import dataclasses
+import os
+from typing import Any, Dict, Optional
+
+import yaml
+
+
+@dataclasses.dataclass(frozen=True)
+class ViTArch:
+    """A ViT architecture: image size, patch, width, depth, heads, MLP width, LayerNorm eps."""
+
+    name: str
+    img_size: int
+    patch: int
+    dim: int
+    depth: int
+    heads: int
+    mlp: int
+    ln_eps: float = 1e-6
+
+    @property
+    def grid(self) -> int:
+        return self.img_size // self.patch
+
+    @property
+    def n_patches(self) -> int:
+        return self.grid * self.grid
+
+    @property
+    def tokens(self) -> int:
+        return self.n_patches + 1
+
+    @property
+    def head_dim(self) -> int:
+        return self.dim // self.heads
+
+    @property
+    def patch_k(self) -> int:
+        return 3 * self.patch * self.patch
+
+    @property
+    def patch_kp(self) -> int:
+        """Patch-GEMM K padded to the 64-deep K-step of the HIP GEMM (SPEC S3)."""
+        return (self.patch_k + 63) // 64 * 64
+
+    def gflop_per_crop(self) -> float:
+        """Algorithmic FLOPs of one crop's forward (SURVEY.md §8d formula), in GFLOP."""
+        n, N, D, L, H, hd, F = self.n_patches, self.tokens, self.dim, self.depth, self.heads, self.head_dim, self.mlp
+        f = 2 * (n * self.patch_k * D + L * (N * D * 3 * D + 2 * H * N * N * hd + N * D * D + 2 * N * D * F))
+        return f / 1e9
+
+
+ARCHS: Dict[str, ViTArch] = {
+    "vit_tiny_patch16_224": ViTArch("vit_tiny_patch16_224", 224, 16, 192, 12, 3, 768),
+    "vit_small_patch16_224": ViTArch("vit_small_patch16_224", 224, 16, 384, 12, 6, 1536),
+    "vit_base_patch16_224": ViTArch("vit_base_patch16_224", 224, 16, 768, 12, 12, 3072),
+    "vit_large_patch14_336": ViTArch("vit_large_patch14_336", 336, 14, 1024, 24, 16, 4096),
+}
+
+
+DEFAULTS: Dict[str, Any] = {
+    "model": {
+        "arch": "vit_base_patch16_224",
+        "dtype": "bf16",                 # bf16 (product) | fp32 (parity mode)
+        "weights": {"seed": 0},
+        "mean": [0.5, 0.5, 0.5],
+        "std": [0.5, 0.5, 0.5],
+    },
+    "particles": {
+        "num": 4096,
+        "motion_std": [4.0, 4.0, 0.02],
+        "scale_range": [0.5, 2.0],
+        "seed": 1234,
+    },
+    "likelihood": {"lambda": 20.0, "weight_bits": 40},
+    "resample": {"method": "systematic"},
+    "input": {"source": "synthetic", "frames": 32, "height": 224, "width": 224,
+              "bbox0": [80, 80, 64, 64], "seed": 7},
+    "distributed": {"world_size": 1},
+}
+
+
+def _merge(base: Dict[str, Any], over: Dict[str, Any]) -> Dict[str, Any]:
+    out = copy.deepcopy(base)
+    for k, v in (over or {}).items():
+        if isinstance(v, dict) and isinstance(out.get(k), dict):
+            out[k] = _merge(out[k], v)
+        else:
+            out[k] = copy.deepcopy(v)
+    return out
+
+
+def load_config(cfg: Optional[Any] = None) -> Dict[str, Any]:
+    """Accept a path to a YAML file, a dict (partial is fine) or None; return the full config dict."""
+    if cfg is None:
+        user = {}
+    elif isinstance(cfg, (str, os.PathLike)):
+        with open(cfg, "r") as fh:
+            user = yaml.safe_load(fh) or {}
+    elif isinstance(cfg, dict):
+        user = cfg
+    else:
+        raise TypeError(f"config must be a path, dict or None, got {type(cfg).__name__}")
+    out = _merge(DEFAULTS, user)
+    arch = out["model"]["arch"]
+    if arch not in ARCHS:
+        raise ValueError(f"unknown model.arch {arch!r}; known: {sorted(ARCHS)}")
+    if out["model"]["dtype"] not in ("bf16", "fp32"):
+        raise ValueError("model.dtype must be 'bf16' or 'fp32'")
+    if out["resample"]["method"] != "systematic":
+        raise ValueError("only resample.method == 'systematic' is defined (SPEC S7)")
+    return out
+
+
+def arch_of(cfg: Dict[str, Any]) -> ViTArch:
+    return ARCHS[cfg["model"]["arch"]]

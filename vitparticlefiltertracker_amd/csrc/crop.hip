@@ -1,0 +1,141 @@
+// Particle crop gather (SPEC S3) and CLS rows (H3).
+//
+// vpf_crop_patches_*: one thread produces 8 consecutive columns of one im2col row (a 16-B bf16 store,
+// rows of Kp columns, fully coalesced across the wave). The frame (150 KB at 224x224) stays L2/L1
+// resident; each output takes 4 bilinear taps. Arithmetic order is SPEC S3's, contraction off, so the
+// fp32 values are bit-identical to oracle/pf_oracle.c and the bf16 values are their RNE rounding.
+#pragma clang fp contract(off)
+#include "vpf_common.h"
+#include "../../include/vpf.h"
+
+using namespace vpf;
+
+struct NormAB { float a[3]; float b[3]; };
+
+__device__ __forceinline__ float frame_tap(const uint8_t* __restrict__ fr, int H, int W, int yy, int xx, int c) {
+    if (yy < 0 || yy >= H || xx < 0 || xx >= W) return 0.0f;
+    return (float)fr[((int64_t)yy * W + xx) * 3 + c];
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(256) void k_crop_patches(const uint8_t* __restrict__ frame, int H, int W,
+                                                      const float* __restrict__ xs,
+                                                      const float* __restrict__ ys,
+                                                      const float* __restrict__ ss, int64_t n_rows,
+                                                      int n_patches, int g, float w0, float h0, int S,
+                                                      int patch, int Kp, NormAB nab,
+                                                      OutT* __restrict__ out) {
+    const int chunks = Kp >> 3;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= n_rows * chunks) return;
+    const int64_t row = tid / chunks;
+    const int ch = (int)(tid - row * chunks);
+    const int64_t p = row / n_patches;
+    const int pi = (int)(row - p * n_patches);
+    const int py = pi / g, px = pi - (pi / g) * g;
+    const float s = ss[p];
+    const float bw = s * w0, bh = s * h0;
+    const float x0 = xs[p] - 0.5f * bw, y0 = ys[p] - 0.5f * bh;
+    const float dx = bw / (float)S, dy = bh / (float)S;
+    const int pp = patch * patch;
+    const int K = 3 * pp;
+    float vals[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int k = ch * 8 + e;
+        float o = 0.0f;
+        if (k < K) {
+            const int c = k / pp;
+            const int r = k - c * pp;
+            const int ky = r / patch, kx = r - (r / patch) * patch;
+            const int oy = py * patch + ky, ox = px * patch + kx;
+            const float sy = (y0 + ((float)oy + 0.5f) * dy) - 0.5f;
+            const float sx = (x0 + ((float)ox + 0.5f) * dx) - 0.5f;
+            const float fy0 = floorf(sy), fx0 = floorf(sx);
+            const float fy = sy - fy0, fx = sx - fx0;
+            const int iy = (int)fy0, ix = (int)fx0;
+            const float p00 = frame_tap(frame, H, W, iy, ix, c), p01 = frame_tap(frame, H, W, iy, ix + 1, c);
+            const float p10 = frame_tap(frame, H, W, iy + 1, ix, c), p11 = frame_tap(frame, H, W, iy + 1, ix + 1, c);
+            const float top = (1.0f - fx) * p00 + fx * p01;
+            const float bot = (1.0f - fx) * p10 + fx * p11;
+            const float v = (1.0f - fy) * top + fy * bot;
+            o = fmaf(v, nab.a[c], nab.b[c]);
+        }
+        vals[e] = o;
+    }
+    OutT* dst = out + row * (int64_t)Kp + ch * 8;
+    if constexpr (sizeof(OutT) == 2) {
+        uint4 pk;
+        pk.x = pack_bf2(vals[0], vals[1]); pk.y = pack_bf2(vals[2], vals[3]);
+        pk.z = pack_bf2(vals[4], vals[5]); pk.w = pack_bf2(vals[6], vals[7]);
+        *reinterpret_cast<uint4*>(dst) = pk;
+    } else {
+        *reinterpret_cast<float4*>(dst) = make_float4(vals[0], vals[1], vals[2], vals[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(vals[4], vals[5], vals[6], vals[7]);
+    }
+}
+
+template <typename OutT>
+static int crop_launch(const uint8_t* frame, int H, int W, const float* particles, int64_t ld, int64_t n,
+                       float w0, float h0, int S, int patch, int Kp, const float* norm_ab_host, OutT* out,
+                       void* stream) {
+    if (H <= 0 || W <= 0 || n < 0 || ld < n || patch <= 0 || S % patch != 0 || Kp % 8 != 0 ||
+        Kp < 3 * patch * patch || !norm_ab_host)
+        return VPF_ERR_ARG;
+    if (n == 0) return 0;
+    NormAB nab;
+    for (int c = 0; c < 3; ++c) { nab.a[c] = norm_ab_host[c]; nab.b[c] = norm_ab_host[3 + c]; }
+    const int g = S / patch;
+    const int64_t rows = n * g * g;
+    const int64_t work = rows * (Kp / 8);
+    const unsigned blocks = (unsigned)((work + 255) / 256);
+    hipLaunchKernelGGL(k_crop_patches<OutT>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, frame, H, W,
+                       particles, particles + ld, particles + 2 * ld, rows, g * g, g, w0, h0, S, patch, Kp,
+                       nab, out);
+    VPF_RETURN_LAUNCH();
+}
+
+VPF_API int vpf_crop_patches_bf16(const uint8_t* frame, int H, int W, const float* particles, int64_t ld,
+                                  int64_t n, float w0, float h0, int S, int patch, int Kp,
+                                  const float* norm_ab_host, uint16_t* out, void* stream) {
+    return crop_launch<uint16_t>(frame, H, W, particles, ld, n, w0, h0, S, patch, Kp, norm_ab_host, out, stream);
+}
+
+VPF_API int vpf_crop_patches_f32(const uint8_t* frame, int H, int W, const float* particles, int64_t ld,
+                                 int64_t n, float w0, float h0, int S, int patch, int Kp,
+                                 const float* norm_ab_host, float* out, void* stream) {
+    return crop_launch<float>(frame, H, W, particles, ld, n, w0, h0, S, patch, Kp, norm_ab_host, out, stream);
+}
+
+// ---------------- CLS rows: tokens[p][0][:] = cls + pos[0] ----------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_cls_rows(T* __restrict__ tok, int64_t n_part, int N, int D,
+                                                  const float* __restrict__ cls, const float* __restrict__ pos) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= n_part * D) return;
+    const int64_t p = tid / D;
+    const int d = (int)(tid - p * D);
+    const float v = cls[d] + pos[d];
+    if constexpr (sizeof(T) == 2) tok[p * (int64_t)N * D + d] = f2bf(v);
+    else tok[p * (int64_t)N * D + d] = v;
+}
+
+VPF_API int vpf_cls_rows_bf16(uint16_t* tokens, int64_t n_part, int N, int D, const float* cls,
+                              const float* pos, void* stream) {
+    if (n_part < 0 || N <= 0 || D <= 0) return VPF_ERR_ARG;
+    if (n_part == 0) return 0;
+    const unsigned blocks = (unsigned)((n_part * D + 255) / 256);
+    hipLaunchKernelGGL(k_cls_rows<uint16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, tokens, n_part, N,
+                       D, cls, pos);
+    VPF_RETURN_LAUNCH();
+}
+
+VPF_API int vpf_cls_rows_f32(float* tokens, int64_t n_part, int N, int D, const float* cls, const float* pos,
+                             void* stream) {
+    if (n_part < 0 || N <= 0 || D <= 0) return VPF_ERR_ARG;
+    if (n_part == 0) return 0;
+    const unsigned blocks = (unsigned)((n_part * D + 255) / 256);
+    hipLaunchKernelGGL(k_cls_rows<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, tokens, n_part, N, D,
+                       cls, pos);
+    VPF_RETURN_LAUNCH();
+}

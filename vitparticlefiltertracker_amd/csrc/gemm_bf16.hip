@@ -1,0 +1,240 @@
+// bf16 GEMM with fused epilogues for the ViT encoder.
+//
+//   C[M][N] = epi( A[M][K] . W[N][K]^T ),  bf16 operands, fp32 accumulation on MFMA.
+//
+// Design (gfx950; MI355X_MICROARCH.md / cdna_hip_programming.md §5):
+//  * 256x256 output tile, BK = 64, 512 threads = 8 waves laid out 2 (M) x 4 (N); each wave owns a
+//    128 (M) x 64 (N) sub-tile = 8 x 4 fragments of v_mfma_f32_16x16x32_bf16 (128 accumulator VGPRs).
+//  * Operands are staged HBM/L2 -> LDS by global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave-instruction,
+//    no VGPR round trip) into a 2-stage LDS ring (2 x 64 KiB). The LDS image is lane-linear; bank
+//    conflicts of the fragment reads (ds_read_b128) are removed by XOR-swizzling the per-lane SOURCE
+//    address: 16-B chunk c of row r lives at physical chunk c ^ ((r >> 1) & 7) (tools/lds_banks.py:
+//    conflict-free for every 16-lane group).
+//  * One barrier per K-step: the DMA for K-tile t+1 is issued right after the barrier and flies while
+//    the 64 MFMAs per wave of tile t run.
+//  * MFMA operands are "swapped" (W fragment as A, activation fragment as B) so the accumulator holds
+//    D[n][m]: each lane owns 4 consecutive output columns of one row. Epilogue: bias (+ exact-erf GELU)
+//    in fp32 on the accumulators, bf16 pack, 8-B writes into a per-wave XOR-swizzled LDS image, then
+//    fully coalesced 16-B row stores (+ 16-B residual reads / position-embedding adds).
+//  * Workgroup -> tile mapping is XCD-aware (bijective remap, cdna_hip_programming.md §5 T1): the blocks
+//    that share an XCD walk consecutive tiles of one 256-row A panel, so the panel is an L2 hit.
+#include "vpf_common.h"
+#include "../../include/vpf.h"
+
+using namespace vpf;
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int NTHREADS = 512;
+constexpr int OPERAND_BYTES = BM * BK * 2;      // 32 KiB per operand tile
+constexpr int STAGE_BYTES = 2 * OPERAND_BYTES;  // A + B
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KiB
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+__device__ __forceinline__ float gelu_erf(float x) {
+    // x * Phi(x) with erfc from Numerical Recipes' erfcc (|relative error| < 1.2e-7 everywhere).
+    const float z = fabsf(x) * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+    float p = 0.17087277f;
+    p = fmaf(p, t, -0.82215223f);
+    p = fmaf(p, t, 1.48851587f);
+    p = fmaf(p, t, -1.13520398f);
+    p = fmaf(p, t, 0.27886807f);
+    p = fmaf(p, t, -0.18628806f);
+    p = fmaf(p, t, 0.09678418f);
+    p = fmaf(p, t, 0.37409196f);
+    p = fmaf(p, t, 1.00002368f);
+    p = fmaf(p, t, -1.26551223f);
+    const float e = fmaf(-z, z, p);
+    const float half_erfc = 0.5f * t * __builtin_amdgcn_exp2f(e * 1.44269504088896341f);
+    const float phi = x >= 0.0f ? 1.0f - half_erfc : half_erfc;
+    return x * phi;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A,
+                                                        const bf16_t* __restrict__ W,
+                                                        const float* __restrict__ bias,
+                                                        const bf16_t* residual,
+                                                        const float* __restrict__ pos, int g2,
+                                                        bf16_t* C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // ---- XCD-aware bijective block -> tile remap ----
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tiles_n = (N + BN - 1) / BN;
+    const int tm = lid / tiles_n, tn = lid - (lid / tiles_n) * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    // ---- per-lane DMA source offsets (bytes, relative to the block's panel base) ----
+    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * K * 2;
+    const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2;
+    uint32_t offA[4], offB[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int g = i * 8 + wid;                 // wave-instruction index: rows [8g, 8g+8)
+        const int row = 8 * g + (lane >> 3);
+        const int pch = lane & 7;
+        const int lch = pch ^ ((row >> 1) & 7);    // logical chunk stored at this physical slot
+        const int ra = min(row, M - 1 - m0);
+        const int rb = min(row, N - 1 - n0);
+        offA[i] = (uint32_t)ra * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
+        offB[i] = (uint32_t)rb * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
+    }
+    auto stage = [&](int buf, int kt) {
+        char* la = smem + buf * STAGE_BYTES;
+        char* lb = la + OPERAND_BYTES;
+        const uint32_t koff = (uint32_t)kt * (BK * 2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int g = i * 8 + wid;
+            __builtin_amdgcn_global_load_lds((gptr_t)(Ablk + offA[i] + koff), (lptr_t)(la + g * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)(Bblk + offB[i] + koff), (lptr_t)(lb + g * 1024), 16, 0, 0);
+        }
+    };
+
+    const int wm = wid >> 2, wn = wid & 3;
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // fragment read addresses (byte offsets inside an operand tile), excluding the ks chunk term
+    const int fr = lane & 15, fq = lane >> 4;
+    const int nk = K / BK;
+    stage(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();   // vmcnt(0) + barrier: tile kt landed for every wave; tile kt-1 fully read
+        if (kt + 1 < nk) stage((kt + 1) & 1, kt + 1);
+        const char* la = smem + (kt & 1) * STAGE_BYTES;
+        const char* lb = la + OPERAND_BYTES;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 a[8], b[4];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = wm * 128 + i * 16 + fr;
+                const int ch = (ks * 4 + fq) ^ ((row >> 1) & 7);
+                a[i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + ch * 16);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = wn * 64 + j * 16 + fr;
+                const int ch = (ks * 4 + fq) ^ ((row >> 1) & 7);
+                b[j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + ch * 16);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
+        }
+    }
+
+    // ---------------- epilogue ----------------
+    __syncthreads();   // every wave is done with the operand ring; reuse it as 8 x 16 KiB images
+    char* img = smem + wid * 16384;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int nl = wn * 64 + j * 16 + fq * 4;     // column (within the block tile) of this lane's 4 values
+        const int ng = n0 + nl;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float v0 = acc[j][i][0] + bv.x, v1 = acc[j][i][1] + bv.y;
+            float v2 = acc[j][i][2] + bv.z, v3 = acc[j][i][3] + bv.w;
+            if constexpr (EPI == VPF_EPI_BIAS_GELU) {
+                v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+            }
+            const int row = i * 16 + fr;              // row within the wave's 128-row image
+            const int c8 = (j * 4 + fq) ^ (row & 15);  // swizzled 8-B chunk
+            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+        }
+    }
+    __syncthreads();
+    const int c16 = lane & 7;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+        const int row = it * 8 + (lane >> 3);
+        uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+        if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+        const int m = m0 + wm * 128 + row;
+        const int n = n0 + wn * 64 + c16 * 8;
+        if (m >= M || n >= N) continue;
+        int64_t orow = m;
+        if constexpr (EPI == VPF_EPI_PATCH) {
+            const int pi = m % g2;
+            orow = (int64_t)(m / g2) * (g2 + 1) + 1 + pi;
+            const float* pr = pos + (int64_t)(1 + pi) * N + n;
+            const float4 p0 = *reinterpret_cast<const float4*>(pr);
+            const float4 p1 = *reinterpret_cast<const float4*>(pr + 4);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const float pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = pack_bf2(bf2f((bf16_t)(w[e] & 0xffff)) + pv[2 * e], bf2f((bf16_t)(w[e] >> 16)) + pv[2 * e + 1]);
+            v = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
+            const uint4 rv = *reinterpret_cast<const uint4*>(residual + (int64_t)m * N + n);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = pack_bf2(bf2f((bf16_t)(w[e] & 0xffff)) + bf2f((bf16_t)(rr[e] & 0xffff)),
+                                bf2f((bf16_t)(w[e] >> 16)) + bf2f((bf16_t)(rr[e] >> 16)));
+            v = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        *reinterpret_cast<uint4*>(C + orow * N + n) = v;
+    }
+}
+
+}  // namespace
+
+VPF_API int vpf_gemm_bf16(const uint16_t* A, const uint16_t* W, const float* bias, const uint16_t* residual,
+                          const float* pos, int patch_rows, uint16_t* C, int64_t M, int64_t N, int64_t K,
+                          int epilogue, void* stream) {
+    if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 8 != 0) return VPF_ERR_ARG;
+    if (M > INT32_MAX / 2 || N > 65536 || K > 65536) return VPF_ERR_ARG;
+    if ((uint64_t)BM * (uint64_t)K * 2 > UINT32_MAX) return VPF_ERR_ARG;
+    if (!A || !W || !bias || !C) return VPF_ERR_ARG;
+    if (epilogue == VPF_EPI_BIAS_RESIDUAL && !residual) return VPF_ERR_ARG;
+    if (epilogue == VPF_EPI_PATCH && (!pos || patch_rows <= 0 || M % patch_rows != 0)) return VPF_ERR_ARG;
+    const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (tiles > INT32_MAX) return VPF_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid((unsigned)tiles), block(NTHREADS);
+    const int m = (int)M, n = (int)N, k = (int)K;
+    const bf16_t* a = A; const bf16_t* w = W; bf16_t* c = C;
+    switch (epilogue) {
+        case VPF_EPI_BIAS:
+            hipLaunchKernelGGL(k_gemm_bf16<VPF_EPI_BIAS>, grid, block, 0, s, a, w, bias, residual, pos, patch_rows, c, m, n, k);
+            break;
+        case VPF_EPI_BIAS_GELU:
+            hipLaunchKernelGGL(k_gemm_bf16<VPF_EPI_BIAS_GELU>, grid, block, 0, s, a, w, bias, residual, pos, patch_rows, c, m, n, k);
+            break;
+        case VPF_EPI_BIAS_RESIDUAL:
+            hipLaunchKernelGGL(k_gemm_bf16<VPF_EPI_BIAS_RESIDUAL>, grid, block, 0, s, a, w, bias, residual, pos, patch_rows, c, m, n, k);
+            break;
+        case VPF_EPI_PATCH:
+            hipLaunchKernelGGL(k_gemm_bf16<VPF_EPI_PATCH>, grid, block, 0, s, a, w, bias, residual, pos, patch_rows, c, m, n, k);
+            break;
+        default:
+            return VPF_ERR_ARG;
+    }
+    VPF_RETURN_LAUNCH();
+}

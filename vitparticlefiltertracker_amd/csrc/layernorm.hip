@@ -1,0 +1,189 @@
+// LayerNorm rows and the fused final-LN -> cosine -> fixed-point weight kernel
+// (H9 + H10, SPEC S4/S5).
+//
+// One wave per row (HBM-bound: 2 bytes in + 2 bytes out per element for bf16). Lane i holds the 4-element
+// chunks i, i+64, i+128, i+192 (D <= 1024, D % 4 == 0) in registers, so the row is read once; mean and
+// variance are two wave reductions over the register copy (two-pass, fp32).
+#include "vpf_common.h"
+#include "../../include/vpf.h"
+
+using namespace vpf;
+
+namespace {
+
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+    static __device__ __forceinline__ void load(const float* p, float v[4]) {
+        const float4 x = *reinterpret_cast<const float4*>(p);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    }
+    static __device__ __forceinline__ void store(float* p, const float v[4]) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+};
+template <> struct Vec4<bf16_t> {
+    static __device__ __forceinline__ void load(const bf16_t* p, float v[4]) {
+        const uint2 x = *reinterpret_cast<const uint2*>(p);
+        v[0] = bf2f((bf16_t)(x.x & 0xffff)); v[1] = bf2f((bf16_t)(x.x >> 16));
+        v[2] = bf2f((bf16_t)(x.y & 0xffff)); v[3] = bf2f((bf16_t)(x.y >> 16));
+    }
+    static __device__ __forceinline__ void store(bf16_t* p, const float v[4]) {
+        *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+    }
+};
+
+// Normalise one row held as up to 4 chunks of 4 per lane. Returns values in v (in place).
+template <typename T>
+__device__ __forceinline__ void ln_row(const T* __restrict__ x, int D, const float* __restrict__ g,
+                                       const float* __restrict__ b, float eps, int lane, float v[16]) {
+    const int nch = D >> 2;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) {
+            Vec4<T>::load(x + 4 * c, v + 4 * i);
+            s += (v[4 * i] + v[4 * i + 1]) + (v[4 * i + 2] + v[4 * i + 3]);
+        } else {
+            v[4 * i] = v[4 * i + 1] = v[4 * i + 2] = v[4 * i + 3] = 0.f;
+        }
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { const float d = v[4 * i + e] - mean; q = fmaf(d, d, q); }
+        }
+    }
+    const float var = wave_sum(q) / (float)D;
+    const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) {
+            const float4 gg = *reinterpret_cast<const float4*>(g + 4 * c);
+            const float4 bb = *reinterpret_cast<const float4*>(b + 4 * c);
+            v[4 * i + 0] = (v[4 * i + 0] - mean) * rstd * gg.x + bb.x;
+            v[4 * i + 1] = (v[4 * i + 1] - mean) * rstd * gg.y + bb.y;
+            v[4 * i + 2] = (v[4 * i + 2] - mean) * rstd * gg.z + bb.z;
+            v[4 * i + 3] = (v[4 * i + 3] - mean) * rstd * gg.w + bb.w;
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_layernorm(const T* __restrict__ x, int64_t rows, int D, int64_t xs,
+                                                   const float* __restrict__ g, const float* __restrict__ b,
+                                                   float eps, T* __restrict__ y, int64_t ys) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    float v[16];
+    ln_row<T>(x + row * xs, D, g, b, eps, lane, v);
+    const int nch = D >> 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) Vec4<T>::store(y + row * ys + 4 * c, v + 4 * i);
+    }
+}
+
+template <typename T, bool DO_LN>
+__global__ __launch_bounds__(256) void k_cls_weight(const T* __restrict__ tok, int64_t n, int N, int D,
+                                                    const float* __restrict__ g, const float* __restrict__ b,
+                                                    float eps, const float* __restrict__ tmpl, float lam,
+                                                    double scale, float* __restrict__ feat,
+                                                    float* __restrict__ sim_out, int64_t* __restrict__ Q) {
+    const int lane = threadIdx.x & 63;
+    const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= n) return;
+    float v[16];
+    const int nch = D >> 2;
+    if constexpr (DO_LN) {
+        ln_row<T>(tok + p * (int64_t)N * D, D, g, b, eps, lane, v);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = lane + 64 * i;
+            if (c < nch) Vec4<T>::load(tok + p * (int64_t)N * D + 4 * c, v + 4 * i);
+        }
+    }
+    float dot = 0.f, nn = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) {
+            const float4 t = *reinterpret_cast<const float4*>(tmpl + 4 * c);
+            dot = fmaf(v[4 * i], t.x, dot); dot = fmaf(v[4 * i + 1], t.y, dot);
+            dot = fmaf(v[4 * i + 2], t.z, dot); dot = fmaf(v[4 * i + 3], t.w, dot);
+            nn = fmaf(v[4 * i], v[4 * i], nn); nn = fmaf(v[4 * i + 1], v[4 * i + 1], nn);
+            nn = fmaf(v[4 * i + 2], v[4 * i + 2], nn); nn = fmaf(v[4 * i + 3], v[4 * i + 3], nn);
+            if (feat) *reinterpret_cast<float4*>(feat + p * D + 4 * c) =
+                make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+        }
+    }
+    dot = wave_sum(dot);
+    nn = wave_sum(nn);
+    if (lane == 0) {
+        const float sim = nn > 0.f ? dot / sqrtf(nn) : 0.f;
+        const float w = fixed_expf(lam * (sim - 1.0f));
+        Q[p] = (int64_t)floor((double)w * scale);
+        if (sim_out) sim_out[p] = sim;
+    }
+}
+
+template <typename T>
+int ln_launch(const T* x, int64_t rows, int D, int64_t x_stride, const float* gamma, const float* beta,
+              float eps, T* y, int64_t y_stride, void* stream) {
+    if (rows < 0 || D <= 0 || D % 4 != 0 || D > 1024 || x_stride < D || y_stride < D) return VPF_ERR_ARG;
+    if (rows == 0) return 0;
+    const unsigned blocks = (unsigned)((rows + 3) / 4);
+    hipLaunchKernelGGL(k_layernorm<T>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, rows, D, x_stride,
+                       gamma, beta, eps, y, y_stride);
+    VPF_RETURN_LAUNCH();
+}
+
+template <typename T>
+int clsw_launch(const T* tokens, int64_t n, int N, int D, const float* gamma, const float* beta, float eps,
+                const float* tmpl, float lam, int bits, float* feat_out, float* sim_out, int64_t* Q,
+                void* stream) {
+    if (n < 0 || N <= 0 || D <= 0 || D % 4 != 0 || D > 1024 || bits < 0 || bits > 62 || !Q || !tmpl)
+        return VPF_ERR_ARG;
+    if (n == 0) return 0;
+    const unsigned blocks = (unsigned)((n + 3) / 4);
+    if (gamma)
+        hipLaunchKernelGGL((k_cls_weight<T, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, tokens, n, N, D,
+                           gamma, beta, eps, tmpl, lam, ldexp(1.0, bits), feat_out, sim_out, Q);
+    else
+        hipLaunchKernelGGL((k_cls_weight<T, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, tokens, n, N,
+                           D, gamma, beta, eps, tmpl, lam, ldexp(1.0, bits), feat_out, sim_out, Q);
+    VPF_RETURN_LAUNCH();
+}
+
+}  // namespace
+
+VPF_API int vpf_layernorm_bf16(const uint16_t* x, int64_t rows, int D, int64_t x_stride, const float* gamma,
+                               const float* beta, float eps, uint16_t* y, int64_t y_stride, void* stream) {
+    return ln_launch<bf16_t>(x, rows, D, x_stride, gamma, beta, eps, y, y_stride, stream);
+}
+VPF_API int vpf_layernorm_f32(const float* x, int64_t rows, int D, int64_t x_stride, const float* gamma,
+                              const float* beta, float eps, float* y, int64_t y_stride, void* stream) {
+    return ln_launch<float>(x, rows, D, x_stride, gamma, beta, eps, y, y_stride, stream);
+}
+VPF_API int vpf_cls_weight_bf16(const uint16_t* tokens, int64_t n, int N, int D, const float* gamma,
+                                const float* beta, float eps, const float* tmpl, float lam, int bits,
+                                float* feat_out, float* sim_out, int64_t* Q, void* stream) {
+    return clsw_launch<bf16_t>(tokens, n, N, D, gamma, beta, eps, tmpl, lam, bits, feat_out, sim_out, Q, stream);
+}
+VPF_API int vpf_cosine_weight_f32(const float* feat, int64_t n, int D, const float* tmpl, float lam, int bits,
+                                  float* sim_out, int64_t* Q, void* stream) {
+    return clsw_launch<float>(feat, n, 1, D, nullptr, nullptr, 0.f, tmpl, lam, bits, nullptr, sim_out, Q, stream);
+}
+VPF_API int vpf_cls_weight_f32(const float* tokens, int64_t n, int N, int D, const float* gamma,
+                               const float* beta, float eps, const float* tmpl, float lam, int bits,
+                               float* feat_out, float* sim_out, int64_t* Q, void* stream) {
+    return clsw_launch<float>(tokens, n, N, D, gamma, beta, eps, tmpl, lam, bits, feat_out, sim_out, Q, stream);
+}

@@ -1,0 +1,151 @@
+"""PyTorch-ROCm custom ops `torch.ops.vpf.*` over the libvpf C-ABI.
+
+Every op is registered for the CUDA (= HIP on ROCm) device only: called with CPU tensors it raises, and
+if libvpf.so is missing it raises — the product path has no CPU fallback (the CPU restatement lives in
+oracle/ and is test infrastructure). Ops write into caller-provided outputs (`Tensor(a!)` out
+arguments), so a whole frame can be captured into one HIP graph (vit.py) with every buffer preallocated.
+Kernels run on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+
+_BF16 = torch.bfloat16
+_F32 = torch.float32
+
+
+def _chk(cond: bool, msg: str) -> None:
+    if not cond:
+        raise ValueError(msg)
+
+
+def _dev(*ts) -> None:
+    for t in ts:
+        if t is not None:
+            _chk(t.is_cuda, "vpf ops run on the GPU only (no CPU fallback); got a CPU tensor")
+            _chk(t.is_contiguous(), "vpf ops expect contiguous tensors")
+
+
+@torch.library.custom_op("vpf::predict_", mutates_args={"particles"}, device_types="cuda")
+def predict_(particles: torch.Tensor, global_begin: int, seed: int, frame: int, motion_std: List[float],
+             width: float, height: float, scale_range: List[float]) -> None:
+    """H1, SPEC S2: in-place random walk on particles float32[3][n]."""
+    _dev(particles)
+    _chk(particles.dtype == _F32 and particles.dim() == 2 and particles.shape[0] == 3, "particles: f32[3][n]")
+    n = particles.shape[1]
+    call("vpf_predict", ptr(particles), n, n, global_begin, seed & (2**64 - 1), frame, motion_std[0],
+         motion_std[1], motion_std[2], width, height, scale_range[0], scale_range[1], stream_ptr())
+
+
+@torch.library.custom_op("vpf::crop_patches", mutates_args={"out"}, device_types="cuda")
+def crop_patches(frame: torch.Tensor, particles: torch.Tensor, box_wh: List[float], img_size: int, patch: int,
+                 norm_ab: List[float], out: torch.Tensor) -> None:
+    """H2+H3 A operand, SPEC S3: out[n*g*g][Kp] (bf16 or f32)."""
+    _dev(frame, particles, out)
+    _chk(frame.dtype == torch.uint8 and frame.dim() == 3 and frame.shape[2] == 3, "frame: u8[H][W][3]")
+    _chk(particles.dtype == _F32 and particles.dim() == 2 and particles.shape[0] == 3, "particles: f32[3][n]")
+    n = particles.shape[1]
+    g = img_size // patch
+    kp = out.shape[1]
+    _chk(out.dim() == 2 and out.shape[0] == n * g * g, "out: [n*g*g][Kp]")
+    ab = (torch.tensor(norm_ab, dtype=torch.float32)).numpy()
+    import ctypes
+    abp = ab.ctypes.data_as(ctypes.c_void_p)
+    name = "vpf_crop_patches_bf16" if out.dtype == _BF16 else "vpf_crop_patches_f32"
+    _chk(out.dtype in (_BF16, _F32), "out dtype must be bf16 or f32")
+    call(name, ptr(frame), frame.shape[0], frame.shape[1], ptr(particles), n, n, box_wh[0], box_wh[1], img_size,
+         patch, kp, abp, ptr(out), stream_ptr())
+
+
+@torch.library.custom_op("vpf::cls_rows_", mutates_args={"tokens"}, device_types="cuda")
+def cls_rows_(tokens: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor) -> None:
+    """H3: tokens[p][0][:] = cls + pos[0]; tokens [n][N][D]."""
+    _dev(tokens, cls, pos)
+    n, N, D = tokens.shape
+    name = "vpf_cls_rows_bf16" if tokens.dtype == _BF16 else "vpf_cls_rows_f32"
+    call(name, ptr(tokens), n, N, D, ptr(cls), ptr(pos), stream_ptr())
+
+
+@torch.library.custom_op("vpf::gemm", mutates_args={"out"}, device_types="cuda")
+def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: Optional[torch.Tensor],
+         pos: Optional[torch.Tensor], patch_rows: int, epilogue: int, out: torch.Tensor) -> None:
+    """H3/H5/H7/H8: out = epilogue(a[M][K] . w[N][K]^T) (bf16 MFMA or fp32 parity mode by dtype)."""
+    _dev(a, w, bias, residual, pos, out)
+    M, K = a.shape
+    N = w.shape[0]
+    _chk(w.shape[1] == K and bias.numel() == N and bias.dtype == _F32, "gemm: shape mismatch")
+    _chk(a.dtype == w.dtype == out.dtype, "gemm: a, w, out must share a dtype")
+    if epilogue == _lib.VPF_EPI_PATCH:
+        _chk(out.numel() >= (M // patch_rows) * (patch_rows + 1) * N, "gemm: patch output too small")
+    else:
+        _chk(out.numel() >= M * N, "gemm: output too small")
+    name = "vpf_gemm_bf16" if a.dtype == _BF16 else "vpf_gemm_f32"
+    call(name, ptr(a), ptr(w), ptr(bias), ptr(residual), ptr(pos), patch_rows, ptr(out), M, N, K, epilogue,
+         stream_ptr())
+
+
+@torch.library.custom_op("vpf::layernorm", mutates_args={"out"}, device_types="cuda")
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor) -> None:
+    """H4: row LayerNorm over the last dim."""
+    _dev(x, gamma, beta, out)
+    D = x.shape[-1]
+    rows = x.numel() // D
+    name = "vpf_layernorm_bf16" if x.dtype == _BF16 else "vpf_layernorm_f32"
+    call(name, ptr(x), rows, D, D, ptr(gamma), ptr(beta), eps, ptr(out), D, stream_ptr())
+
+
+@torch.library.custom_op("vpf::attention", mutates_args={"out"}, device_types="cuda")
+def attention(qkv: torch.Tensor, heads: int, out: torch.Tensor) -> None:
+    """H6: qkv [B][N][3D] -> out [B][N][D]."""
+    _dev(qkv, out)
+    B, N, D3 = qkv.shape
+    D = D3 // 3
+    hd = D // heads
+    name = "vpf_attention_bf16" if qkv.dtype == _BF16 else "vpf_attention_f32"
+    call(name, ptr(qkv), ptr(out), B, N, heads, hd, hd ** -0.5, stream_ptr())
+
+
+@torch.library.custom_op("vpf::cls_weight", mutates_args={"Q", "feat", "sim"}, device_types="cuda")
+def cls_weight(tokens: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, tmpl: torch.Tensor,
+               lam: float, bits: int, Q: torch.Tensor, feat: Optional[torch.Tensor],
+               sim: Optional[torch.Tensor]) -> None:
+    """H9+H10: final LN of CLS rows -> cosine with template -> Q = floor(exp(lam(sim-1)) 2^bits)."""
+    _dev(tokens, gamma, beta, tmpl, Q, feat, sim)
+    n, N, D = tokens.shape
+    _chk(Q.dtype == torch.int64 and Q.numel() == n, "Q: int64[n]")
+    name = "vpf_cls_weight_bf16" if tokens.dtype == _BF16 else "vpf_cls_weight_f32"
+    call(name, ptr(tokens), n, N, D, ptr(gamma), ptr(beta), eps, ptr(tmpl), lam, bits, ptr(feat), ptr(sim),
+         ptr(Q), stream_ptr())
+
+
+@torch.library.custom_op("vpf::cosine_weight", mutates_args={"Q"}, device_types="cuda")
+def cosine_weight(feat: torch.Tensor, tmpl: torch.Tensor, lam: float, bits: int, Q: torch.Tensor) -> None:
+    """H10 alone: Q from explicit fp32 features [n][D] and a unit template."""
+    _dev(feat, tmpl, Q)
+    n, D = feat.shape
+    _chk(feat.dtype == _F32 and Q.dtype == torch.int64 and Q.numel() == n, "cosine_weight: f32[n][D] -> int64[n]")
+    call("vpf_cosine_weight_f32", ptr(feat), n, D, ptr(tmpl), lam, bits, 0, ptr(Q), stream_ptr())
+
+
+@torch.library.custom_op("vpf::shard_stats", mutates_args={"out_T", "out_sums"}, device_types="cuda")
+def shard_stats(Q: torch.Tensor, particles: torch.Tensor, out_T: torch.Tensor, out_sums: torch.Tensor) -> None:
+    """H11: out_T int64[1] = sum Q, out_sums f64[3] = sum Q*(x, y, s)."""
+    _dev(Q, particles, out_T, out_sums)
+    n = Q.numel()
+    call("vpf_shard_stats", ptr(Q), ptr(particles), particles.shape[1], n, ptr(out_T), ptr(out_sums), stream_ptr())
+
+
+@torch.library.custom_op("vpf::resample", mutates_args={"anc", "states", "cdf_ws"}, device_types="cuda")
+def resample(Q: torch.Tensor, global_begin: int, offset: int, total: int, P: int, U: int, uniform: bool,
+             slot_begin: int, slot_end: int, particles: torch.Tensor, anc: torch.Tensor, states: torch.Tensor,
+             cdf_ws: torch.Tensor) -> None:
+    """H12: ancestors + states of slots [slot_begin, slot_end) whose positions fall in this shard."""
+    _dev(Q, particles, anc, states, cdf_ws)
+    n_local = Q.numel()
+    call("vpf_resample", ptr(Q), n_local, global_begin, offset, total, P, U, int(uniform), slot_begin, slot_end,
+         ptr(particles), particles.shape[1], ptr(anc), ptr(states), states.shape[1], ptr(cdf_ws), stream_ptr())

@@ -1,0 +1,150 @@
+"""`Tracker` — the per-frame loop the reference drives from main.py ("integrates the Vision Transformer
+(ViT) architecture with a Particle Filter to achieve precise object position tracking",
+/root/reference/README.md:3; "provide the input data ... configure ... config.yaml ... output the tracked
+positions", README.md:42). SPEC.md S8 / SURVEY.md §8a H13-H14.
+
+    t = Tracker("config.yaml")        # or a dict, or None for the defaults
+    t.init(frame0, (x, y, w, h))      # template feature from the bbox crop (H13)
+    for f in frames: x, y, s = t.track(f)
+
+Per frame: predict (eager launch; its frame index is a kernel argument) -> [HIP graph replay: crop+ViT
+-> final LN -> cosine -> Q] -> shard stats (+ 32-B all-gather across ranks) -> estimate -> resample
+(+ chunk all-gather across ranks). The only host synchronisation is reading the shard statistics.
+"""
+from __future__ import annotations
+
+import os
+from typing import Iterable, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import arch_of, load_config
+from .particle_filter import ParticleFilter
+from .vit import ViTEngine
+from .weights import make_vit_weights
+
+
+def _dist_info(rank, world_size, group):
+    if rank is not None and world_size is not None:
+        return int(rank), int(world_size), group
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group), group
+    return 0, 1, None
+
+
+class Tracker:
+    def __init__(self, cfg=None, device=None, rank: Optional[int] = None, world_size: Optional[int] = None,
+                 group=None, use_graph: bool = True, weights=None):
+        self.cfg = load_config(cfg)
+        if not torch.cuda.is_available():
+            raise _lib.VPFError("Tracker runs on the HIP device only; the CPU restatement is oracle/ (tests)")
+        self.rank, self.world_size, self.group = _dist_info(rank, world_size, group)
+        if device is None:
+            local = int(os.environ.get("LOCAL_RANK", self.rank % max(1, torch.cuda.device_count())))
+            device = torch.device("cuda", local)
+        self.device = torch.device(device)
+        torch.cuda.set_device(self.device)
+        c = self.cfg
+        self.arch = arch_of(c)
+        P = int(c["particles"]["num"])
+        if P % self.world_size:
+            raise ValueError("particles.num must be divisible by the world size")
+        self.n_local = P // self.world_size
+        w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
+        self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, max(1, self.n_local),
+                                c["model"]["mean"], c["model"]["std"])
+        self.lam = float(c["likelihood"]["lambda"])
+        self.bits = int(c["likelihood"]["weight_bits"])
+        self.use_graph = bool(use_graph)
+        self.pf: Optional[ParticleFilter] = None
+        self.template: Optional[torch.Tensor] = None
+        self.box_wh: Optional[Tuple[float, float]] = None
+        self._frame_dev: Optional[torch.Tensor] = None
+        self._frame_host: Optional[torch.Tensor] = None
+        self._graph: Optional[torch.cuda.CUDAGraph] = None
+        self.frame_index = 0
+
+    # ------------------------------------------------------------------ frames
+    def _upload(self, frame) -> torch.Tensor:
+        if isinstance(frame, torch.Tensor) and frame.is_cuda:
+            src = frame.to(torch.uint8)
+            if self._frame_dev is None or self._frame_dev.shape != src.shape:
+                self._frame_dev = torch.empty_like(src)
+                self._graph = None
+            self._frame_dev.copy_(src)
+            return self._frame_dev
+        arr = np.ascontiguousarray(frame.cpu().numpy() if isinstance(frame, torch.Tensor) else frame, dtype=np.uint8)
+        if arr.ndim != 3 or arr.shape[2] != 3:
+            raise ValueError("frame must be uint8[H][W][3]")
+        if self._frame_dev is None or tuple(self._frame_dev.shape) != arr.shape:
+            self._frame_dev = torch.empty(arr.shape, dtype=torch.uint8, device=self.device)
+            self._frame_host = torch.empty(arr.shape, dtype=torch.uint8).pin_memory()
+            self._graph = None
+        self._frame_host.numpy()[...] = arr
+        self._frame_dev.copy_(self._frame_host, non_blocking=True)
+        return self._frame_dev
+
+    # ------------------------------------------------------------------ H13
+    def init(self, frame, bbox) -> None:
+        """Template from the bbox (x, y, w, h) crop at scale 1; particles reset to the bbox centre."""
+        fd = self._upload(frame)
+        bx, by, bw, bh = (float(v) for v in bbox)
+        self.box_wh = (bw, bh)
+        cx, cy = bx + 0.5 * bw, by + 0.5 * bh
+        one = torch.tensor([[cx], [cy], [1.0]], dtype=torch.float32, device=self.device)
+        f = self.engine.features(fd, one, self.box_wh)[0].clone()
+        self.template = (f / f.norm()).contiguous()
+        c = self.cfg
+        if self.pf is None:
+            self.pf = ParticleFilter(int(c["particles"]["num"]), (cx, cy, 1.0), c["particles"]["motion_std"],
+                                     c["particles"]["scale_range"], int(c["particles"]["seed"]), self.device,
+                                     (fd.shape[0], fd.shape[1]), self.lam, self.bits, self.rank, self.world_size,
+                                     self.group)
+        else:
+            self.pf.height, self.pf.width = fd.shape[0], fd.shape[1]
+            self.pf.reset((cx, cy, 1.0))
+        self._graph = None
+        self.frame_index = 0
+
+    # ------------------------------------------------------------------ H14
+    def _features_to_weights(self) -> None:
+        self.engine.forward_weights(self._frame_dev, self.pf.particles, self.box_wh, self.template, self.lam,
+                                    self.bits)
+
+    def _capture(self) -> None:
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._features_to_weights()   # warm-up outside capture
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._features_to_weights()
+        self._graph = g
+
+    def weigh(self) -> None:
+        """Crop + ViT + weights for the current particles and uploaded frame (graph replay when enabled)."""
+        if self.use_graph:
+            if self._graph is None:
+                self._capture()
+            self._graph.replay()
+        else:
+            self._features_to_weights()
+        self.pf.set_weights(self.engine.Q[: self.n_local])
+
+    def track(self, frame) -> Tuple[float, float, float]:
+        if self.pf is None:
+            raise RuntimeError("call init(frame, bbox) first")
+        self._upload(frame)
+        self.frame_index += 1
+        self.pf.predict(self.frame_index)
+        self.weigh()
+        est = self.pf.estimate()
+        self.pf.resample()
+        return est
+
+    def run(self, frames: Iterable) -> np.ndarray:
+        return np.array([self.track(f) for f in frames], dtype=np.float64)
