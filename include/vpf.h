@@ -33,6 +33,8 @@ extern "C" {
 #define VPF_EPI_BIAS_GELU 1     /* C = gelu_erf(A W^T + bias)                                      */
 #define VPF_EPI_BIAS_RESIDUAL 2 /* C = R + (A W^T + bias); R may alias C                          */
 #define VPF_EPI_PATCH 3         /* row m -> token (m/g2)*(g2+1)+1+m%g2; C = A W^T + bias + pos[1+m%g2] */
+#define VPF_EPI_LN 4            /* LayerNorm folded: C = rstd_m (A W'^T) - rstd_m mean_m colsum + bias'     */
+#define VPF_EPI_LN_GELU 5       /* gelu_erf of the above                                                  */
 
 /* library identity: returns a static string "libvpf <version> gfx950" */
 const char* vpf_version(void);
@@ -60,16 +62,28 @@ int vpf_cls_rows_f32(float* tokens, int64_t n_part, int N, int D, const float* c
                      void* stream);
 
 /* H3/H5/H7/H8: C[M][N] = epilogue(A[M][K] * W[N][K]^T). bf16 in/out, fp32 accumulate (MFMA).
- * bias: fp32[N]; residual: bf16[M][N] (EPI_BIAS_RESIDUAL, may alias C); pos: fp32[g2+1][N] (EPI_PATCH,
- * with g2 = patch_rows, M % g2 == 0). Requires K % 64 == 0, N % 8 == 0. */
-int vpf_gemm_bf16(const uint16_t* A, const uint16_t* W, const float* bias, const uint16_t* residual,
-                  const float* pos, int patch_rows, uint16_t* C, int64_t M, int64_t N, int64_t K,
+ * Row m of A at A + m*lda; row m of C (and of the residual, which has C's layout) at C + m*ldc.
+ * bias: fp32[N]; residual: bf16 (EPI_BIAS_RESIDUAL, may alias C); pos: fp32[g2+1][N] (EPI_PATCH, with
+ * g2 = patch_rows, M % g2 == 0); EPI_LN / EPI_LN_GELU (LayerNorm folded into the GEMM, A = the raw
+ * residual stream): row_stats fp32[M][2] = {mean, rstd} of A's rows (vpf_row_stats_*), W = W * diag(gamma),
+ * colsum fp32[N] = sum_k W[n][k] (of the bf16 W), bias = b + W_orig beta. Unused pointers may be NULL.
+ * Requires K % 64 == 0, N % 8 == 0, lda % 8 == 0, ldc % 8 == 0. */
+int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, const float* bias,
+                  const uint16_t* residual, const float* pos, int patch_rows, const float* row_stats,
+                  const float* colsum, uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                   int epilogue, void* stream);
 /* fp32 parity mode: same contract with fp32 tensors (exact-f32 MFMA, v_mfma_f32_32x32x2_f32).
- * Requires K % 32 == 0. */
-int vpf_gemm_f32(const float* A, const float* W, const float* bias, const float* residual,
-                 const float* pos, int patch_rows, float* C, int64_t M, int64_t N, int64_t K,
-                 int epilogue, void* stream);
+ * Requires K % 32 == 0, lda % 4 == 0, ldc % 4 == 0. */
+int vpf_gemm_f32(const float* A, int64_t lda, const float* W, const float* bias, const float* residual,
+                 const float* pos, int patch_rows, const float* row_stats, const float* colsum, float* C,
+                 int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue, void* stream);
+
+/* H4 (folded form): out[r] = {mean, rstd = 1/sqrt(var + eps)} of row r (at x + r*x_stride), fp32.
+ * bf16: D % 8 == 0; fp32: D % 4 == 0; D <= 1024. */
+int vpf_row_stats_bf16(const uint16_t* x, int64_t rows, int D, int64_t x_stride, float eps, float* out,
+                       void* stream);
+int vpf_row_stats_f32(const float* x, int64_t rows, int D, int64_t x_stride, float eps, float* out,
+                      void* stream);
 
 /* H4: y = LayerNorm(x) per row (fp32 statistics). Row r of x at x + r*x_stride; D % 4 == 0, D <= 1024. */
 int vpf_layernorm_bf16(const uint16_t* x, int64_t rows, int D, int64_t x_stride, const float* gamma,
@@ -78,11 +92,12 @@ int vpf_layernorm_f32(const float* x, int64_t rows, int D, int64_t x_stride, con
                       const float* beta, float eps, float* y, int64_t y_stride, void* stream);
 
 /* H6: per (particle, head) softmax(q k^T * scale) v. qkv: [B][N][3][H][hd], out: [B][N][H][hd].
- * hd == 64, N <= 640. */
+ * Only the first q_rows queries of every particle are computed (q_rows = N: all; 1: the CLS row, used by
+ * the last encoder layer whose other rows feed nothing). hd == 64, N <= 640 (f32: N <= 256). */
 int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd,
-                       float scale, void* stream);
+                       float scale, int q_rows, void* stream);
 int vpf_attention_f32(const float* qkv, float* out, int64_t B, int N, int H, int hd, float scale,
-                      void* stream);
+                      int q_rows, void* stream);
 
 /* H9+H10: final LayerNorm of each particle's CLS row (tokens + p*N*D), cosine similarity with the
  * unit template `tmpl`, w = exp(lam (sim - 1)), Q = floor(w 2^bits) (SPEC S5).

@@ -93,12 +93,12 @@ def test_gemm_bf16(M, N, K, epi):
     R = (torch.randn(M, N, device=DEV)).to(torch.bfloat16) if epi == 2 else None
     out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     Rin = R.clone() if R is not None else None
-    vpf().gemm(A, W, bias, Rin, None, 0, epi, out)
+    vpf().gemm(A, W, bias, Rin, None, 0, None, None, epi, out)
     ref = _epi_ref(A.float() @ W.float().t(), bias, epi, R)
     torch.testing.assert_close(out.float(), ref, rtol=1.6e-2, atol=1e-2)
     if epi == 2:   # in-place residual (out aliases the residual), as the encoder uses it
         h = R.clone()
-        vpf().gemm(A, W, bias, h, None, 0, epi, h)
+        vpf().gemm(A, W, bias, h, None, 0, None, None, epi, h)
         assert torch.equal(h, out)
 
 
@@ -108,7 +108,7 @@ def test_gemm_bf16_asymmetric_identity():
     A = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
     W = (torch.arange(N * K, device=DEV, dtype=torch.float32).reshape(N, K) % 97 - 48).to(torch.bfloat16)
     out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    vpf().gemm(A, W, torch.zeros(N, device=DEV), None, None, 0, 0, out)
+    vpf().gemm(A, W, torch.zeros(N, device=DEV), None, None, 0, None, None, 0, out)
     assert torch.equal(out, W.t().contiguous())
 
 
@@ -122,7 +122,7 @@ def test_gemm_patch_epilogue(dtype):
     bias = torch.randn(D, device=DEV) * 0.1
     pos = torch.randn(g2 + 1, D, device=DEV) * 0.1
     out = torch.full((n, g2 + 1, D), 7.0, device=DEV, dtype=dtype)
-    vpf().gemm(A, W, bias, None, pos, g2, 3, out)
+    vpf().gemm(A, W, bias, None, pos, g2, None, None, 3, out)
     ref = ((A.double() @ W.double().t()) + bias.double()).reshape(n, g2, D) + pos[1:].double()
     tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(out[:, 1:].double(), ref, **tol)
@@ -141,10 +141,60 @@ def test_gemm_f32(M, N, K, epi):
     bias = torch.randn(N, device=DEV)
     R = torch.randn(M, N, device=DEV) if epi == 2 else None
     out = torch.empty(M, N, device=DEV)
-    vpf().gemm(A, W, bias, R, None, 0, epi, out)
+    vpf().gemm(A, W, bias, R, None, 0, None, None, epi, out)
     acc = A.double() @ W.double().t() + bias.double()
     ref = Fn.gelu(acc) if epi == 1 else (acc + R.double() if epi == 2 else acc)
     torch.testing.assert_close(out.double(), ref, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_gemm_layernorm_fold(dtype, gelu):
+    """EPI_LN / EPI_LN_GELU on the raw rows == LayerNorm -> GEMM(+GELU) (SPEC S4 folded form)."""
+    torch.manual_seed(11 + gelu)
+    M, D, N = 777, 768, 2304
+    h = (torch.randn(M, D, device=DEV) * 1.3 + 0.4).to(dtype)
+    g = 1 + 0.2 * torch.randn(D, device=DEV)
+    be = 0.1 * torch.randn(D, device=DEV)
+    W = torch.randn(N, D, device=DEV) / D ** 0.5
+    b = 0.1 * torch.randn(N, device=DEV)
+    Wg = (W * g).to(dtype)
+    colsum = Wg.float().sum(1)
+    bias = b + W @ be
+    st = torch.empty(M, 2, device=DEV)
+    vpf().row_stats(h, 1e-6, st)
+    ref_st = torch.stack([h.double().mean(1), 1 / torch.sqrt(h.double().var(1, unbiased=False) + 1e-6)], 1)
+    torch.testing.assert_close(st.double(), ref_st, rtol=1e-5, atol=1e-5)
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    vpf().gemm(h, Wg, bias, None, None, 0, st, colsum, 5 if gelu else 4, out)
+    ref = Fn.layer_norm(h.double(), (D,), g.double(), be.double(), 1e-6) @ W.double().t() + b.double()
+    if gelu:
+        ref = Fn.gelu(ref)
+    tol = dict(rtol=2e-2, atol=3e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(out.double(), ref, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gemm_strided_rows(dtype):
+    """a / out / residual as row-strided views (the last layer's CLS rows of the token tensor)."""
+    torch.manual_seed(12)
+    n, Ntok, D, F = 300, 197, 768, 3072
+    tok = torch.randn(n, Ntok, D, device=DEV).to(dtype)
+    hid = torch.empty(n, F, device=DEV, dtype=dtype)
+    W1 = (torch.randn(F, D, device=DEV) / D ** 0.5).to(dtype)
+    b1 = torch.randn(F, device=DEV) * 0.1
+    cls = tok.view(n, Ntok * D)[:, :D]
+    vpf().gemm(cls, W1, b1, None, None, 0, None, None, 1, hid)
+    ref = Fn.gelu(tok[:, 0].double() @ W1.double().t() + b1.double())
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(hid.double(), ref, **tol)
+    W2 = (torch.randn(D, F, device=DEV) / F ** 0.5).to(dtype)
+    b2 = torch.randn(D, device=DEV) * 0.1
+    before = tok.clone()
+    vpf().gemm(hid, W2, b2, cls, None, 0, None, None, 2, cls)
+    ref2 = before[:, 0].double() + (hid.double() @ W2.double().t() + b2.double())
+    torch.testing.assert_close(tok[:, 0].double(), ref2, **tol)
+    assert torch.equal(tok[:, 1:], before[:, 1:])          # non-CLS rows untouched
 
 
 # ------------------------------------------------------------------ LayerNorm
@@ -160,6 +210,17 @@ def test_layernorm(rows, D, dtype):
     ref = Fn.layer_norm(x.double(), (D,), g.double(), b.double(), 1e-6)
     tol = dict(rtol=1e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(y.double(), ref, **tol)
+    # row-strided input / output views
+    big = torch.zeros(rows, 3 * D, device=DEV, dtype=dtype)
+    big[:, D:2 * D] = x
+    ys = torch.zeros(rows, 2 * D, device=DEV, dtype=dtype)
+    vpf().layernorm(big[:, D:2 * D], g, b, 1e-6, ys[:, :D])
+    assert torch.equal(ys[:, :D], y) and torch.all(ys[:, D:] == 0)
+    if D % 8 == 0:
+        st = torch.empty(rows, 2, device=DEV)
+        vpf().row_stats(big[:, D:2 * D], 1e-6, st)
+        ref_st = torch.stack([x.double().mean(1), 1 / torch.sqrt(x.double().var(1, unbiased=False) + 1e-6)], 1)
+        torch.testing.assert_close(st.double(), ref_st, rtol=1e-5, atol=1e-5)
 
 
 # ------------------------------------------------------------------ attention
@@ -169,11 +230,25 @@ def test_attention_bf16(B, N, H):
     D = 64 * H
     qkv = (torch.randn(B, N, 3 * D, device=DEV) * 1.5).to(torch.bfloat16)
     out = torch.empty(B, N, D, device=DEV, dtype=torch.bfloat16)
-    vpf().attention(qkv, H, out)
+    vpf().attention(qkv, H, N, out)
     q, k, v = qkv.float().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = torch.softmax((q @ k.transpose(-1, -2)) * 0.125, -1) @ v
     ref = ref.transpose(1, 2).reshape(B, N, D)
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_attention_q_rows(dtype):
+    torch.manual_seed(3)
+    B, N, H = 4, 197, 3
+    D = 64 * H
+    qkv = torch.randn(B, N, 3 * D, device=DEV).to(dtype)
+    full = torch.empty(B, N, D, device=DEV, dtype=dtype)
+    vpf().attention(qkv, H, N, full)
+    part = torch.full((B, N, D), 5.0, device=DEV, dtype=dtype)
+    vpf().attention(qkv, H, 1, part)
+    assert torch.equal(part[:, 0], full[:, 0])
+    assert torch.all(part[:, 1:] == 5.0)
 
 
 @pytest.mark.parametrize("B,N,H", [(2, 197, 3), (1, 50, 2)])
@@ -182,7 +257,7 @@ def test_attention_f32(B, N, H):
     D = 64 * H
     qkv = torch.randn(B, N, 3 * D, device=DEV)
     out = torch.empty(B, N, D, device=DEV)
-    vpf().attention(qkv, H, out)
+    vpf().attention(qkv, H, N, out)
     q, k, v = qkv.double().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = (torch.softmax((q @ k.transpose(-1, -2)) * 0.125, -1) @ v).transpose(1, 2).reshape(B, N, D)
     torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-5)

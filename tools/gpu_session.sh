@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU session: each GPU step under its own time limit; stop at the first crash / timeout / abort.
+# Usage: tools/gpu_session.sh <tag> [tests] [smoke] [bench] [prof]
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+ok_or_stop() {  # rc 0 (pass) / 1 (test failures) continue; anything else = crash/timeout -> stop
+  local rc=$1 what=$2
+  echo "[$what] rc=$rc" | tee -a $OUT/status.txt
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $what (rc=$rc)" | tee -a $OUT/status.txt; exit $rc; fi
+}
+rocm-smi --showproductname > $OUT/gpu.txt 2>&1 || true
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 1500 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 -rf > $OUT/pytest_gpu.log 2>&1
+      ok_or_stop $? tests; tail -30 $OUT/pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+      ok_or_stop $? smoke; tail -5 $OUT/smoke.log ;;
+    bench)
+      timeout -k 10 900 python bench.py --steps 5 --warmup 2 > $OUT/bench.log 2>&1
+      ok_or_stop $? bench; tail -3 $OUT/bench.log ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/prof.log 2>&1
+      ok_or_stop $? prof; tail -3 $OUT/prof.log ;;
+  esac
+done
+echo done | tee -a $OUT/status.txt

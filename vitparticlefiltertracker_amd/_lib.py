@@ -28,6 +28,8 @@ VPF_EPI_BIAS = 0
 VPF_EPI_BIAS_GELU = 1
 VPF_EPI_BIAS_RESIDUAL = 2
 VPF_EPI_PATCH = 3
+VPF_EPI_LN = 4
+VPF_EPI_LN_GELU = 5
 
 _P, _I64, _I32, _U64, _U32, _F32 = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint64,
                                     ctypes.c_uint32, ctypes.c_float)
@@ -39,12 +41,14 @@ SIGNATURES = {
     "vpf_crop_patches_f32": [_P, _I32, _I32, _P, _I64, _I64, _F32, _F32, _I32, _I32, _I32, _P, _P, _P],
     "vpf_cls_rows_bf16": [_P, _I64, _I32, _I32, _P, _P, _P],
     "vpf_cls_rows_f32": [_P, _I64, _I32, _I32, _P, _P, _P],
-    "vpf_gemm_bf16": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I64, _I64, _I32, _P],
-    "vpf_gemm_f32": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I64, _I64, _I32, _P],
+    "vpf_gemm_bf16": [_P, _I64, _P, _P, _P, _P, _I32, _P, _P, _P, _I64, _I64, _I64, _I64, _I32, _P],
+    "vpf_gemm_f32": [_P, _I64, _P, _P, _P, _P, _I32, _P, _P, _P, _I64, _I64, _I64, _I64, _I32, _P],
+    "vpf_row_stats_bf16": [_P, _I64, _I32, _I64, _F32, _P, _P],
+    "vpf_row_stats_f32": [_P, _I64, _I32, _I64, _F32, _P, _P],
     "vpf_layernorm_bf16": [_P, _I64, _I32, _I64, _P, _P, _F32, _P, _I64, _P],
     "vpf_layernorm_f32": [_P, _I64, _I32, _I64, _P, _P, _F32, _P, _I64, _P],
-    "vpf_attention_bf16": [_P, _P, _I64, _I32, _I32, _I32, _F32, _P],
-    "vpf_attention_f32": [_P, _P, _I64, _I32, _I32, _I32, _F32, _P],
+    "vpf_attention_bf16": [_P, _P, _I64, _I32, _I32, _I32, _F32, _I32, _P],
+    "vpf_attention_f32": [_P, _P, _I64, _I32, _I32, _I32, _F32, _I32, _P],
     "vpf_cls_weight_bf16": [_P, _I64, _I32, _I32, _P, _P, _F32, _P, _F32, _I32, _P, _P, _P, _P],
     "vpf_cls_weight_f32": [_P, _I64, _I32, _I32, _P, _P, _F32, _P, _F32, _I32, _P, _P, _P, _P],
     "vpf_cosine_weight_f32": [_P, _I64, _I32, _P, _F32, _I32, _P, _P, _P],

@@ -40,7 +40,7 @@ __device__ __forceinline__ bf16x4 ds_read_tr(const char* lds_base, int byte_off)
 }
 
 __global__ __launch_bounds__(256) void k_attn_bf16(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                   int N, int H, float scale_log2) {
+                                                   int N, int H, float scale_log2, int q_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int NP = (N + 63) & ~63;
     char* Ks = smem;
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void k_attn_bf16(const bf16_t* __restrict__ qk
     __syncthreads();
 
     const int l32 = lane & 31, hh = lane >> 5;
-    const int nstrips = (N + 31) >> 5;
+    const int nstrips = (q_rows + 31) >> 5;
     for (int strip = wid; strip < nstrips; strip += 4) {
         const int q = strip * 32 + l32;
         // Q^T fragments (B operand): lane holds Q[q][16ks + 8hh + j]
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_attn_bf16(const bf16_t* __restrict__ qk
         }
         l += __shfl_xor(l, 32, 64);
         const float inv = 1.0f / l;
-        if (q < N) {
+        if (q < q_rows) {
             bf16_t* orow = out + (row0 + q) * D + h * HD;
 #pragma unroll
             for (int g4 = 0; g4 < 4; ++g4) {
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void k_attn_bf16(const bf16_t* __restrict__ qk
 
 // ---------------- fp32 parity path ----------------
 __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ qkv, float* __restrict__ out, int N,
-                                                  int H, float scale) {
+                                                  int H, float scale, int q_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* Ks = reinterpret_cast<float*>(smem);
     float* Vs = Ks + N * HD;
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ qkv,
         Vs[idx] = qbase[(int64_t)r * 3 * D + 2 * D + c];
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < N; q += blockDim.x) {
+    for (int q = threadIdx.x; q < q_rows; q += blockDim.x) {
         float qv[HD];
         for (int c = 0; c < HD; ++c) qv[c] = qbase[(int64_t)q * 3 * D + c];
         float mx = -INFINITY;
@@ -210,8 +210,9 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ qkv,
 }  // namespace
 
 VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd, float scale,
-                               void* stream) {
-    if (B < 0 || N <= 0 || N > 640 || H <= 0 || hd != HD || B * H > INT32_MAX) return VPF_ERR_ARG;
+                               int q_rows, void* stream) {
+    if (B < 0 || N <= 0 || N > 640 || H <= 0 || hd != HD || B * H > INT32_MAX || q_rows < 1 || q_rows > N)
+        return VPF_ERR_ARG;
     if (B == 0) return 0;
     const int NP = (N + 63) & ~63;
     const size_t lds = (size_t)NP * ROWB * 2;
@@ -222,13 +223,14 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
         attr_set = true;
     }
     hipLaunchKernelGGL(k_attn_bf16, dim3((unsigned)(B * H)), dim3(256), lds, (hipStream_t)stream, qkv, out, N, H,
-                       scale_log2);
+                       scale_log2, q_rows);
     VPF_RETURN_LAUNCH();
 }
 
 VPF_API int vpf_attention_f32(const float* qkv, float* out, int64_t B, int N, int H, int hd, float scale,
-                              void* stream) {
-    if (B < 0 || N <= 0 || N > 256 || H <= 0 || hd != HD || B * H > INT32_MAX) return VPF_ERR_ARG;
+                              int q_rows, void* stream) {
+    if (B < 0 || N <= 0 || N > 256 || H <= 0 || hd != HD || B * H > INT32_MAX || q_rows < 1 || q_rows > N)
+        return VPF_ERR_ARG;
     if (B == 0) return 0;
     const size_t lds = (size_t)N * HD * 4 * 2;
     static bool attr_set = false;
@@ -237,6 +239,6 @@ VPF_API int vpf_attention_f32(const float* qkv, float* out, int64_t B, int N, in
         attr_set = true;
     }
     hipLaunchKernelGGL(k_attn_f32, dim3((unsigned)(B * H)), dim3(256), lds, (hipStream_t)stream, qkv, out, N, H,
-                       scale);
+                       scale, q_rows);
     VPF_RETURN_LAUNCH();
 }

@@ -58,12 +58,14 @@ __device__ __forceinline__ float gelu_erf(float x) {
 }
 
 template <int EPI>
-__global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A,
+__global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W,
                                                         const float* __restrict__ bias,
                                                         const bf16_t* residual,
                                                         const float* __restrict__ pos, int g2,
-                                                        bf16_t* C, int M, int N, int K) {
+                                                        const float2* __restrict__ stats,
+                                                        const float* __restrict__ colsum,
+                                                        bf16_t* C, int ldc, int M, int N, int K) {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     const int m0 = tm * BM, n0 = tn * BN;
 
     // ---- per-lane DMA source offsets (bytes, relative to the block's panel base) ----
-    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * K * 2;
+    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * lda * 2;
     const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2;
     uint32_t offA[4], offB[4];
 #pragma unroll
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         const int lch = pch ^ ((row >> 1) & 7);    // logical chunk stored at this physical slot
         const int ra = min(row, M - 1 - m0);
         const int rb = min(row, N - 1 - n0);
-        offA[i] = (uint32_t)ra * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
+        offA[i] = (uint32_t)ra * (uint32_t)(lda * 2) + (uint32_t)(lch * 16);
         offB[i] = (uint32_t)rb * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
     }
     auto stage = [&](int buf, int kt) {
@@ -145,17 +147,37 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     // ---------------- epilogue ----------------
     __syncthreads();   // every wave is done with the operand ring; reuse it as 8 x 16 KiB images
     char* img = smem + wid * 16384;
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    float2 rs[8];   // LN-fold: per-row (rstd, -rstd*mean) of this lane's 8 rows
+    if constexpr (LN) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int m = m0 + wm * 128 + i * 16 + fr;
+            const float2 st = m < M ? stats[m] : make_float2(0.f, 0.f);
+            rs[i] = make_float2(st.y, -st.y * st.x);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int nl = wn * 64 + j * 16 + fq * 4;     // column (within the block tile) of this lane's 4 values
         const int ng = n0 + nl;
-        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f), cv = make_float4(0.f, 0.f, 0.f, 0.f);
         if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
+        if constexpr (LN) { if (ng < N) cv = *reinterpret_cast<const float4*>(colsum + ng); }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            float v0 = acc[j][i][0] + bv.x, v1 = acc[j][i][1] + bv.y;
-            float v2 = acc[j][i][2] + bv.z, v3 = acc[j][i][3] + bv.w;
-            if constexpr (EPI == VPF_EPI_BIAS_GELU) {
+            float v0, v1, v2, v3;
+            if constexpr (LN) {
+                // LN(x) W^T + b = rstd (x W'^T) - rstd mean colsum(W') + b'   (gamma folded into W', beta into b')
+                v0 = fmaf(rs[i].x, acc[j][i][0], fmaf(rs[i].y, cv.x, bv.x));
+                v1 = fmaf(rs[i].x, acc[j][i][1], fmaf(rs[i].y, cv.y, bv.y));
+                v2 = fmaf(rs[i].x, acc[j][i][2], fmaf(rs[i].y, cv.z, bv.z));
+                v3 = fmaf(rs[i].x, acc[j][i][3], fmaf(rs[i].y, cv.w, bv.w));
+            } else {
+                v0 = acc[j][i][0] + bv.x; v1 = acc[j][i][1] + bv.y;
+                v2 = acc[j][i][2] + bv.z; v3 = acc[j][i][3] + bv.w;
+            }
+            if constexpr (EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU) {
                 v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
             }
             const int row = i * 16 + fr;              // row within the wave's 128-row image
@@ -189,7 +211,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             v = make_uint4(o[0], o[1], o[2], o[3]);
         }
         if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
-            const uint4 rv = *reinterpret_cast<const uint4*>(residual + (int64_t)m * N + n);
+            const uint4 rv = *reinterpret_cast<const uint4*>(residual + (int64_t)m * ldc + n);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
             const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
             uint32_t o[4];
@@ -199,42 +221,42 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                                 bf2f((bf16_t)(w[e] >> 16)) + bf2f((bf16_t)(rr[e] >> 16)));
             v = make_uint4(o[0], o[1], o[2], o[3]);
         }
-        *reinterpret_cast<uint4*>(C + orow * N + n) = v;
+        *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
     }
 }
 
 }  // namespace
 
-VPF_API int vpf_gemm_bf16(const uint16_t* A, const uint16_t* W, const float* bias, const uint16_t* residual,
-                          const float* pos, int patch_rows, uint16_t* C, int64_t M, int64_t N, int64_t K,
+#define VPF_GEMM_LAUNCH(E)                                                                                   \
+    hipLaunchKernelGGL(k_gemm_bf16<E>, grid, block, 0, s, A, (int)lda, W, bias, residual, pos, patch_rows,         \
+                       reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k)
+
+VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, const float* bias,
+                          const uint16_t* residual, const float* pos, int patch_rows, const float* row_stats,
+                          const float* colsum, uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                           int epilogue, void* stream) {
-    if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 8 != 0) return VPF_ERR_ARG;
-    if (M > INT32_MAX / 2 || N > 65536 || K > 65536) return VPF_ERR_ARG;
-    if ((uint64_t)BM * (uint64_t)K * 2 > UINT32_MAX) return VPF_ERR_ARG;
+    if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 8 != 0 || lda < K || lda % 8 != 0 || ldc < N ||
+        ldc % 8 != 0)
+        return VPF_ERR_ARG;
+    if (M > INT32_MAX / 2 || N > 65536 || K > 65536 || lda > INT32_MAX / 2 || ldc > INT32_MAX / 2) return VPF_ERR_ARG;
+    if ((uint64_t)BM * (uint64_t)lda * 2 > UINT32_MAX) return VPF_ERR_ARG;
     if (!A || !W || !bias || !C) return VPF_ERR_ARG;
     if (epilogue == VPF_EPI_BIAS_RESIDUAL && !residual) return VPF_ERR_ARG;
     if (epilogue == VPF_EPI_PATCH && (!pos || patch_rows <= 0 || M % patch_rows != 0)) return VPF_ERR_ARG;
+    if ((epilogue == VPF_EPI_LN || epilogue == VPF_EPI_LN_GELU) && (!row_stats || !colsum)) return VPF_ERR_ARG;
     const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     if (tiles > INT32_MAX) return VPF_ERR_ARG;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)tiles), block(NTHREADS);
     const int m = (int)M, n = (int)N, k = (int)K;
-    const bf16_t* a = A; const bf16_t* w = W; bf16_t* c = C;
     switch (epilogue) {
-        case VPF_EPI_BIAS:
-            hipLaunchKernelGGL(k_gemm_bf16<VPF_EPI_BIAS>, grid, block, 0, s, a, w, bias, residual, pos, patch_rows, c, m, n, k);
-            break;
-        case VPF_EPI_BIAS_GELU:
-            hipLaunchKernelGGL(k_gemm_bf16<VPF_EPI_BIAS_GELU>, grid, block, 0, s, a, w, bias, residual, pos, patch_rows, c, m, n, k);
-            break;
-        case VPF_EPI_BIAS_RESIDUAL:
-            hipLaunchKernelGGL(k_gemm_bf16<VPF_EPI_BIAS_RESIDUAL>, grid, block, 0, s, a, w, bias, residual, pos, patch_rows, c, m, n, k);
-            break;
-        case VPF_EPI_PATCH:
-            hipLaunchKernelGGL(k_gemm_bf16<VPF_EPI_PATCH>, grid, block, 0, s, a, w, bias, residual, pos, patch_rows, c, m, n, k);
-            break;
-        default:
-            return VPF_ERR_ARG;
+        case VPF_EPI_BIAS: VPF_GEMM_LAUNCH(VPF_EPI_BIAS); break;
+        case VPF_EPI_BIAS_GELU: VPF_GEMM_LAUNCH(VPF_EPI_BIAS_GELU); break;
+        case VPF_EPI_BIAS_RESIDUAL: VPF_GEMM_LAUNCH(VPF_EPI_BIAS_RESIDUAL); break;
+        case VPF_EPI_PATCH: VPF_GEMM_LAUNCH(VPF_EPI_PATCH); break;
+        case VPF_EPI_LN: VPF_GEMM_LAUNCH(VPF_EPI_LN); break;
+        case VPF_EPI_LN_GELU: VPF_GEMM_LAUNCH(VPF_EPI_LN_GELU); break;
+        default: return VPF_ERR_ARG;
     }
     VPF_RETURN_LAUNCH();
 }

@@ -135,6 +135,75 @@ __global__ __launch_bounds__(256) void k_cls_weight(const T* __restrict__ tok, i
     }
 }
 
+// Row statistics for the LayerNorm folded into the next GEMM (vpf_gemm_bf16 EPI_LN*): out[r] = {mean, rstd}.
+// Half a wave (32 lanes) per row, 16-B loads, two-pass variance on the register copy; grid-stride.
+template <typename T>
+__global__ __launch_bounds__(256) void k_row_stats(const T* __restrict__ x, int64_t rows, int D, int64_t xs,
+                                                   float eps, float2* __restrict__ out) {
+    constexpr int EPC = 16 / sizeof(T);               // elements per 16-B chunk
+    constexpr int MAXC = 1024 / EPC / 32;             // chunks per lane for D <= 1024
+    const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+    const int nch = D / EPC;
+    // wave-uniform loop over row pairs: lanes 0-31 take row 2p, lanes 32-63 row 2p+1
+    for (int64_t pr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); 2 * pr < rows; pr += (int64_t)gridDim.x * 4) {
+        const int64_t row = 2 * pr + half;
+        const bool valid = row < rows;
+        float v[MAXC][EPC];
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < MAXC; ++i) {
+            const int c = l32 + 32 * i;
+            if (valid && c < nch) {
+                const uint4 u = *reinterpret_cast<const uint4*>(x + row * xs + c * EPC);
+                if constexpr (sizeof(T) == 2) {
+                    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[i][2 * e] = bf2f((bf16_t)(w[e] & 0xffff));
+                        v[i][2 * e + 1] = bf2f((bf16_t)(w[e] >> 16));
+                    }
+                } else {
+                    v[i][0] = __uint_as_float(u.x); v[i][1] = __uint_as_float(u.y);
+                    v[i][2] = __uint_as_float(u.z); v[i][3] = __uint_as_float(u.w);
+                }
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) s += v[i][e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) v[i][e] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        const float mean = s / (float)D;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < MAXC; ++i) {
+            const int c = l32 + 32 * i;
+            if (c < nch) {
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) { const float d = v[i][e] - mean; q = fmaf(d, d, q); }
+            }
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+        if (valid && l32 == 0) out[row] = make_float2(mean, 1.0f / sqrtf(q / (float)D + eps));
+    }
+}
+
+template <typename T>
+int stats_launch(const T* x, int64_t rows, int D, int64_t x_stride, float eps, float* out, void* stream) {
+    constexpr int EPC = 16 / sizeof(T);
+    if (rows < 0 || D <= 0 || D % EPC != 0 || D > 1024 || x_stride < D || x_stride % EPC != 0 || !out)
+        return VPF_ERR_ARG;
+    if (rows == 0) return 0;
+    const int64_t want = (rows + 7) / 8;
+    const unsigned blocks = (unsigned)(want < 8192 ? want : 8192);
+    hipLaunchKernelGGL(k_row_stats<T>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, rows, D, x_stride, eps,
+                       reinterpret_cast<float2*>(out));
+    VPF_RETURN_LAUNCH();
+}
+
 template <typename T>
 int ln_launch(const T* x, int64_t rows, int D, int64_t x_stride, const float* gamma, const float* beta,
               float eps, T* y, int64_t y_stride, void* stream) {
@@ -172,6 +241,14 @@ VPF_API int vpf_layernorm_bf16(const uint16_t* x, int64_t rows, int D, int64_t x
 VPF_API int vpf_layernorm_f32(const float* x, int64_t rows, int D, int64_t x_stride, const float* gamma,
                               const float* beta, float eps, float* y, int64_t y_stride, void* stream) {
     return ln_launch<float>(x, rows, D, x_stride, gamma, beta, eps, y, y_stride, stream);
+}
+VPF_API int vpf_row_stats_bf16(const uint16_t* x, int64_t rows, int D, int64_t x_stride, float eps, float* out,
+                               void* stream) {
+    return stats_launch<bf16_t>(x, rows, D, x_stride, eps, out, stream);
+}
+VPF_API int vpf_row_stats_f32(const float* x, int64_t rows, int D, int64_t x_stride, float eps, float* out,
+                              void* stream) {
+    return stats_launch<float>(x, rows, D, x_stride, eps, out, stream);
 }
 VPF_API int vpf_cls_weight_bf16(const uint16_t* tokens, int64_t n, int N, int D, const float* gamma,
                                 const float* beta, float eps, const float* tmpl, float lam, int bits,

@@ -71,43 +71,78 @@ def cls_rows_(tokens: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor) -> Non
     call(name, ptr(tokens), n, N, D, ptr(cls), ptr(pos), stream_ptr())
 
 
+def _rows(t: torch.Tensor, what: str):
+    """(rows, row stride) of a 2-D row-major view whose rows may be strided (last dim contiguous)."""
+    _chk(t.dim() == 2 and t.stride(1) == 1, f"{what}: expected a 2-D view with unit column stride")
+    return t.shape[0], t.stride(0)
+
+
 @torch.library.custom_op("vpf::gemm", mutates_args={"out"}, device_types="cuda")
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: Optional[torch.Tensor],
-         pos: Optional[torch.Tensor], patch_rows: int, epilogue: int, out: torch.Tensor) -> None:
-    """H3/H5/H7/H8: out = epilogue(a[M][K] . w[N][K]^T) (bf16 MFMA or fp32 parity mode by dtype)."""
-    _dev(a, w, bias, residual, pos, out)
-    M, K = a.shape
+         pos: Optional[torch.Tensor], patch_rows: int, row_stats: Optional[torch.Tensor],
+         colsum: Optional[torch.Tensor], epilogue: int, out: torch.Tensor) -> None:
+    """H3/H5/H7/H8: out = epilogue(a[M][K] . w[N][K]^T) (bf16 MFMA or fp32 parity mode by dtype).
+
+    `a`, `out` (and `residual`, which must share `out`'s row stride) are 2-D views whose rows may be strided
+    (e.g. the CLS rows of the token tensor). EPI_PATCH takes `out` as the flat token buffer."""
+    _dev(w, bias, pos, row_stats, colsum)
+    for t in (a, out, residual):
+        if t is not None:
+            _chk(t.is_cuda, "vpf ops run on the GPU only (no CPU fallback); got a CPU tensor")
+    M, lda = _rows(a, "gemm a")
+    K = a.shape[1]
     N = w.shape[0]
     _chk(w.shape[1] == K and bias.numel() == N and bias.dtype == _F32, "gemm: shape mismatch")
     _chk(a.dtype == w.dtype == out.dtype, "gemm: a, w, out must share a dtype")
     if epilogue == _lib.VPF_EPI_PATCH:
-        _chk(out.numel() >= (M // patch_rows) * (patch_rows + 1) * N, "gemm: patch output too small")
+        _chk(out.is_contiguous() and out.numel() >= (M // patch_rows) * (patch_rows + 1) * N,
+             "gemm: patch output too small")
+        ldc = N
     else:
-        _chk(out.numel() >= M * N, "gemm: output too small")
+        Mo, ldc = _rows(out, "gemm out")
+        _chk(Mo == M and out.shape[1] == N, "gemm: output shape")
+    if residual is not None:
+        _chk(_rows(residual, "gemm residual") == (M, ldc), "gemm: residual must match out's layout")
+    if epilogue in (_lib.VPF_EPI_LN, _lib.VPF_EPI_LN_GELU):
+        _chk(row_stats is not None and row_stats.numel() >= 2 * M and colsum is not None and colsum.numel() == N,
+             "gemm: LN epilogue needs row_stats[M][2] and colsum[N]")
     name = "vpf_gemm_bf16" if a.dtype == _BF16 else "vpf_gemm_f32"
-    call(name, ptr(a), ptr(w), ptr(bias), ptr(residual), ptr(pos), patch_rows, ptr(out), M, N, K, epilogue,
-         stream_ptr())
+    call(name, ptr(a), lda, ptr(w), ptr(bias), ptr(residual), ptr(pos), patch_rows, ptr(row_stats), ptr(colsum),
+         ptr(out), ldc, M, N, K, epilogue, stream_ptr())
+
+
+@torch.library.custom_op("vpf::row_stats", mutates_args={"out"}, device_types="cuda")
+def row_stats(x: torch.Tensor, eps: float, out: torch.Tensor) -> None:
+    """H4 (folded): out[r] = (mean, rstd) of row r of the 2-D (row-strided) view x."""
+    _dev(out)
+    _chk(x.is_cuda, "vpf ops run on the GPU only")
+    rows, xs = _rows(x, "row_stats x")
+    _chk(out.dtype == _F32 and out.numel() >= 2 * rows, "row_stats: out f32[rows][2]")
+    name = "vpf_row_stats_bf16" if x.dtype == _BF16 else "vpf_row_stats_f32"
+    call(name, ptr(x), rows, x.shape[1], xs, eps, ptr(out), stream_ptr())
 
 
 @torch.library.custom_op("vpf::layernorm", mutates_args={"out"}, device_types="cuda")
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor) -> None:
-    """H4: row LayerNorm over the last dim."""
-    _dev(x, gamma, beta, out)
-    D = x.shape[-1]
-    rows = x.numel() // D
+    """H4: row LayerNorm over the last dim of 2-D (row-strided) views x -> out."""
+    _dev(gamma, beta)
+    _chk(x.is_cuda and out.is_cuda, "vpf ops run on the GPU only")
+    rows, xs = _rows(x, "layernorm x")
+    ro, ys = _rows(out, "layernorm out")
+    _chk(ro == rows and out.shape[1] == x.shape[1], "layernorm: shape")
     name = "vpf_layernorm_bf16" if x.dtype == _BF16 else "vpf_layernorm_f32"
-    call(name, ptr(x), rows, D, D, ptr(gamma), ptr(beta), eps, ptr(out), D, stream_ptr())
+    call(name, ptr(x), rows, x.shape[1], xs, ptr(gamma), ptr(beta), eps, ptr(out), ys, stream_ptr())
 
 
 @torch.library.custom_op("vpf::attention", mutates_args={"out"}, device_types="cuda")
-def attention(qkv: torch.Tensor, heads: int, out: torch.Tensor) -> None:
-    """H6: qkv [B][N][3D] -> out [B][N][D]."""
+def attention(qkv: torch.Tensor, heads: int, q_rows: int, out: torch.Tensor) -> None:
+    """H6: qkv [B][N][3D] -> out [B][N][D]; only the first q_rows queries of each particle."""
     _dev(qkv, out)
     B, N, D3 = qkv.shape
     D = D3 // 3
     hd = D // heads
     name = "vpf_attention_bf16" if qkv.dtype == _BF16 else "vpf_attention_f32"
-    call(name, ptr(qkv), ptr(out), B, N, heads, hd, hd ** -0.5, stream_ptr())
+    call(name, ptr(qkv), ptr(out), B, N, heads, hd, hd ** -0.5, q_rows, stream_ptr())
 
 
 @torch.library.custom_op("vpf::cls_weight", mutates_args={"Q", "feat", "sim"}, device_types="cuda")

@@ -101,17 +101,38 @@ class ViTEngine:
         self.b_pe = f32(weights["patch_embed.bias"])
         self.cls = f32(weights["cls_token"])
         self.pos = f32(weights["pos_embed"])
+        # bf16 product mode folds each pre-GEMM LayerNorm into the GEMM (vpf_gemm_bf16 EPI_LN*):
+        # W' = W diag(gamma) (bf16), colsum = row sums of the rounded W', b' = b + W beta; the GEMM then
+        # reads the raw residual stream and the epilogue applies the per-row (mean, rstd). fp32 parity mode
+        # keeps the explicit LayerNorm kernel (the oracle's operation order).
+        self.fold_ln = self.dt == torch.bfloat16
+
+        def folded(wname, bname, gname, bename):
+            Wf = weights[wname].float()
+            g, be = weights[gname].float(), weights[bename].float()
+            Wg = (Wf * g.unsqueeze(0)).to(dt)
+            colsum = Wg.float().sum(dim=1)
+            bias = weights[bname].float() + Wf @ be
+            return Wg.to(dev).contiguous(), f32(bias), f32(colsum)
+
         self.layers = []
         for l in range(A.depth):
             p = f"blocks.{l}."
-            self.layers.append({
+            L = {
                 "n1g": f32(weights[p + "norm1.weight"]), "n1b": f32(weights[p + "norm1.bias"]),
-                "wqkv": mat(weights[p + "attn.qkv.weight"]), "bqkv": f32(weights[p + "attn.qkv.bias"]),
                 "wproj": mat(weights[p + "attn.proj.weight"]), "bproj": f32(weights[p + "attn.proj.bias"]),
                 "n2g": f32(weights[p + "norm2.weight"]), "n2b": f32(weights[p + "norm2.bias"]),
-                "wfc1": mat(weights[p + "mlp.fc1.weight"]), "bfc1": f32(weights[p + "mlp.fc1.bias"]),
                 "wfc2": mat(weights[p + "mlp.fc2.weight"]), "bfc2": f32(weights[p + "mlp.fc2.bias"]),
-            })
+            }
+            if self.fold_ln:
+                L["wqkv"], L["bqkv"], L["cqkv"] = folded(p + "attn.qkv.weight", p + "attn.qkv.bias",
+                                                         p + "norm1.weight", p + "norm1.bias")
+                L["wfc1"], L["bfc1"], L["cfc1"] = folded(p + "mlp.fc1.weight", p + "mlp.fc1.bias",
+                                                         p + "norm2.weight", p + "norm2.bias")
+            else:
+                L["wqkv"], L["bqkv"] = mat(weights[p + "attn.qkv.weight"]), f32(weights[p + "attn.qkv.bias"])
+                L["wfc1"], L["bfc1"] = mat(weights[p + "mlp.fc1.weight"]), f32(weights[p + "mlp.fc1.bias"])
+            self.layers.append(L)
         self.ng = f32(weights["norm.weight"])
         self.nb = f32(weights["norm.bias"])
         self._alloc(self.batch)
@@ -129,6 +150,7 @@ class ViTEngine:
         self.hid_flat = torch.empty(hid_elems, device=dev, dtype=dt)
         self.hid = self.hid_flat[: n * N * F].view(n * N, F)
         self.patches = self.hid_flat[: n * A.n_patches * A.patch_kp].view(n * A.n_patches, A.patch_kp)
+        self.stats = torch.empty(n * N, 2, device=dev, dtype=torch.float32)
         self.Q = torch.empty(n, device=dev, dtype=torch.int64)
         self.feat = torch.empty(n, D, device=dev, dtype=torch.float32)
         self.sim = torch.empty(n, device=dev, dtype=torch.float32)
@@ -142,29 +164,53 @@ class ViTEngine:
         _run(T, "crop_patches", vpf.crop_patches, frame, particles, [float(box_wh[0]), float(box_wh[1])],
              A.img_size, A.patch, self.norm_ab, patches)
         h = self.h[:n]
-        _run(T, "gemm_patch", vpf.gemm, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches,
+        _run(T, "gemm_patch", vpf.gemm, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches, None, None,
              _lib.VPF_EPI_PATCH, h)
         _run(T, "cls_rows", vpf.cls_rows_, h, self.cls, self.pos)
 
     def encoder(self, n: int) -> None:
+        """L pre-norm blocks on h[:n]. The last block only needs the CLS rows after its attention (the
+        final LN reads nothing else), so its attention computes q_rows = 1 and its proj / MLP run on the
+        n strided CLS rows (outputs identical to the full block's CLS rows)."""
         A = self.arch
-        D, N = A.dim, A.tokens
-        h = self.h[:n]
-        x = self.x[:n]
+        D, N, F = A.dim, A.tokens, A.mlp
+        T = self.timer
+        h2 = self.h[:n].view(n * N, D)
+        x2 = self.x[:n].view(n * N, D)
         qkv = self.qkv[:n]
         hid = self.hid[: n * N]
-        h2 = h.view(n * N, D)
-        x2 = x.view(n * N, D)
-        T = self.timer
-        for L in self.layers:
-            _run(T, "layernorm", vpf.layernorm, h, L["n1g"], L["n1b"], A.ln_eps, x)
-            _run(T, "gemm_qkv", vpf.gemm, x2, L["wqkv"], L["bqkv"], None, None, 0, _lib.VPF_EPI_BIAS,
-                 qkv.view(n * N, 3 * D))
-            _run(T, "attention", vpf.attention, qkv, A.heads, x)
-            _run(T, "gemm_proj", vpf.gemm, x2, L["wproj"], L["bproj"], h2, None, 0, _lib.VPF_EPI_BIAS_RESIDUAL, h2)
-            _run(T, "layernorm", vpf.layernorm, h, L["n2g"], L["n2b"], A.ln_eps, x)
-            _run(T, "gemm_fc1", vpf.gemm, x2, L["wfc1"], L["bfc1"], None, None, 0, _lib.VPF_EPI_BIAS_GELU, hid)
-            _run(T, "gemm_fc2", vpf.gemm, hid, L["wfc2"], L["bfc2"], h2, None, 0, _lib.VPF_EPI_BIAS_RESIDUAL, h2)
+        st = self.stats[: n * N]
+        hc = self.h[:n].view(n, N * D)[:, :D]       # CLS rows (row stride N*D)
+        xc = self.x[:n].view(n, N * D)[:, :D]
+        hidc = self.hid[:n]
+        stc = self.stats[:n]
+        BIAS, GELU, RES = _lib.VPF_EPI_BIAS, _lib.VPF_EPI_BIAS_GELU, _lib.VPF_EPI_BIAS_RESIDUAL
+        LNE, LNG = _lib.VPF_EPI_LN, _lib.VPF_EPI_LN_GELU
+        fold = self.fold_ln
+        if fold:
+            _run(T, "row_stats", vpf.row_stats, h2, A.ln_eps, st)
+        for l, L in enumerate(self.layers):
+            last = l == len(self.layers) - 1
+            if fold:
+                _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, st, L["cqkv"], LNE,
+                     qkv.view(n * N, 3 * D))
+            else:
+                _run(T, "layernorm", vpf.layernorm, h2, L["n1g"], L["n1b"], A.ln_eps, x2)
+                _run(T, "gemm_qkv", vpf.gemm, x2, L["wqkv"], L["bqkv"], None, None, 0, None, None, BIAS,
+                     qkv.view(n * N, 3 * D))
+            _run(T, "attention", vpf.attention, qkv, A.heads, 1 if last else N, self.x[:n])
+            hh, xx, hd_, ss = (hc, xc, hidc, stc) if last else (h2, x2, hid, st)
+            tag = "_cls" if last else ""
+            _run(T, "gemm_proj" + tag, vpf.gemm, xx, L["wproj"], L["bproj"], hh, None, 0, None, None, RES, hh)
+            if fold:
+                _run(T, "row_stats", vpf.row_stats, hh, A.ln_eps, ss)
+                _run(T, "gemm_fc1" + tag, vpf.gemm, hh, L["wfc1"], L["bfc1"], None, None, 0, ss, L["cfc1"], LNG, hd_)
+            else:
+                _run(T, "layernorm", vpf.layernorm, hh, L["n2g"], L["n2b"], A.ln_eps, xx)
+                _run(T, "gemm_fc1" + tag, vpf.gemm, xx, L["wfc1"], L["bfc1"], None, None, 0, None, None, GELU, hd_)
+            _run(T, "gemm_fc2" + tag, vpf.gemm, hd_, L["wfc2"], L["bfc2"], hh, None, 0, None, None, RES, hh)
+            if fold and not last:
+                _run(T, "row_stats", vpf.row_stats, h2, A.ln_eps, st)
 
     def weights_from_tokens(self, n: int, tmpl: torch.Tensor, lam: float, bits: int, want_feat: bool = False):
         _run(self.timer, "cls_weight", vpf.cls_weight, self.h[:n], self.ng, self.nb, self.arch.ln_eps, tmpl,
