@@ -1,0 +1,342 @@
+// GEMM lab (design aid, not product): main-loop pipelining variants of the 256x256x64 bf16 MFMA GEMM at the
+// ViT-B/16 encoder shapes (M = 4096 x 197 rows), timed in ONE process with interleaved rounds
+// (cdna_hip_programming.md §5.4 rule 24) on random data, outputs cross-checked against variant 0.
+//
+//   V0  product structure: 2-stage LDS ring, one __syncthreads per K-tile, all 8 glds issued up front.
+//   V1  V0 + glds issue spread between MFMA groups + s_setprio around MFMA clusters.
+//   V2  ping-pong: waves 4-7 run one barrier behind waves 0-3 (one wave of each group per SIMD), so each
+//       SIMD alternates a wave in its MFMA segment with a wave in its LDS-read/DMA-issue segment.
+//       Segment = 64-deep K-tile; waves 0-3 issue all DMA.
+//   V3  ping-pong with 32-deep segments; both groups issue their share of the DMA in their first segment.
+//
+// Build/run: make -C tools/gemm_lab run   (GPU box)
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+typedef unsigned short bf16_t;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1); } } while (0)
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int OPB = BM * BK * 2, STB = 2 * OPB, LDSB = 2 * STB;
+
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+    __bf16 a = (__bf16)lo, b = (__bf16)hi;
+    return (uint32_t)__builtin_bit_cast(unsigned short, a) | ((uint32_t)__builtin_bit_cast(unsigned short, b) << 16);
+}
+
+struct Ctx {
+    int m0, n0, wid, lane, wm, wn, fr, fq;
+    const char* Ablk; const char* Bblk;
+};
+
+__device__ __forceinline__ Ctx make_ctx(const bf16_t* A, const bf16_t* W, int M, int N, int K, int wm, int wn) {
+    Ctx c;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tiles_n = (N + BN - 1) / BN;
+    const int tm = lid / tiles_n, tn = lid - tm * tiles_n;
+    c.m0 = tm * BM; c.n0 = tn * BN;
+    c.lane = threadIdx.x & 63;
+    c.wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.wm = wm; c.wn = wn; c.fr = c.lane & 15; c.fq = c.lane >> 4;
+    c.Ablk = reinterpret_cast<const char*>(A) + (size_t)c.m0 * K * 2;
+    c.Bblk = reinterpret_cast<const char*>(W) + (size_t)c.n0 * K * 2;
+    return c;
+}
+
+// byte offset (within the block panel) of the 16-B piece lane `lane` moves for wave-instruction g (rows 8g..8g+7)
+__device__ __forceinline__ uint32_t dma_off(int g, int lane, int rows_left, int K) {
+    const int row = 8 * g + (lane >> 3);
+    const int lch = (lane & 7) ^ ((row >> 1) & 7);
+    return (uint32_t)min(row, rows_left) * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
+}
+
+__device__ __forceinline__ void dma(const char* base, uint32_t off, char* lds) {
+    __builtin_amdgcn_global_load_lds((gptr_t)(base + off), (lptr_t)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ void read_frags(const char* la, const char* lb, int ks, const Ctx& c, bf16x8 a[8], bf16x8 b[4]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int row = c.wm * 128 + i * 16 + c.fr;
+        a[i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + (((ks * 4 + c.fq) ^ ((row >> 1) & 7)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = c.wn * 64 + j * 16 + c.fr;
+        b[j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + (((ks * 4 + c.fq) ^ ((row >> 1) & 7)) << 4));
+    }
+}
+
+__device__ __forceinline__ void mfma32(f32x4 acc[4][8], const bf16x8 a[8], const bf16x8 b[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
+}
+
+__device__ __forceinline__ void epilogue(char* smem, f32x4 acc[4][8], const Ctx& c, const float* bias, bf16_t* C,
+                                         int M, int N) {
+    __syncthreads();
+    char* img = smem + c.wid * 16384;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ng = c.n0 + c.wn * 64 + j * 16 + c.fq * 4;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = i * 16 + c.fr;
+            const int c8 = (j * 4 + c.fq) ^ (row & 15);
+            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
+                make_uint2(pack_bf2(acc[j][i][0] + bv.x, acc[j][i][1] + bv.y), pack_bf2(acc[j][i][2] + bv.z, acc[j][i][3] + bv.w));
+        }
+    }
+    __syncthreads();
+    const int c16 = c.lane & 7;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+        const int row = it * 8 + (c.lane >> 3);
+        uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+        if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+        const int m = c.m0 + c.wm * 128 + row, n = c.n0 + c.wn * 64 + c16 * 8;
+        if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * N + n) = v;
+    }
+}
+
+// ---------------------------------------------------------------- V0 / V1
+template <bool SPREAD>
+__global__ __launch_bounds__(512) void k_v01(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                             const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[LDSB];
+    const int wid0 = threadIdx.x >> 6;
+    Ctx c = make_ctx(A, W, M, N, K, wid0 >> 2, wid0 & 3);
+    uint32_t oa[4], ob[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        oa[i] = dma_off(i * 8 + c.wid, c.lane, M - 1 - c.m0, K);
+        ob[i] = dma_off(i * 8 + c.wid, c.lane, N - 1 - c.n0, K);
+    }
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = K / BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        dma(c.Ablk, oa[i], smem + (i * 8 + c.wid) * 1024);
+        dma(c.Bblk, ob[i], smem + OPB + (i * 8 + c.wid) * 1024);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();
+        const char* la = smem + (kt & 1) * STB;
+        const char* lb = la + OPB;
+        char* na = smem + ((kt + 1) & 1) * STB;
+        const uint32_t koff = (uint32_t)(kt + 1) * (BK * 2);
+        const bool pre = kt + 1 < nk;
+        if (!SPREAD && pre) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                dma(c.Ablk, oa[i] + koff, na + (i * 8 + c.wid) * 1024);
+                dma(c.Bblk, ob[i] + koff, na + OPB + (i * 8 + c.wid) * 1024);
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 a[8], b[4];
+            read_frags(la, lb, ks, c, a, b);
+            if (SPREAD) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
+                if (SPREAD && pre) {
+                    const int g = ks * 4 + j;          // 8 DMA pieces over 8 MFMA groups
+                    if (g < 4) dma(c.Ablk, oa[g] + koff, na + (g * 8 + c.wid) * 1024);
+                    else dma(c.Bblk, ob[g - 4] + koff, na + OPB + ((g - 4) * 8 + c.wid) * 1024);
+                }
+            }
+            if (SPREAD) __builtin_amdgcn_s_setprio(0);
+        }
+    }
+    epilogue(smem, acc, c, bias, C, M, N);
+}
+
+// ---------------------------------------------------------------- V2 / V3 ping-pong
+// SEG32 = false: one load + one compute segment per 64-deep K-tile, group 0 issues all DMA.
+// SEG32 = true : two (32-deep) segment pairs per K-tile, every wave issues its 8 DMA pieces in segment 0.
+template <bool SEG32>
+__global__ __launch_bounds__(512) void k_pp(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                            const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[LDSB];
+    const int wid0 = threadIdx.x >> 6;
+    const int grp = wid0 >> 2;
+    Ctx c = make_ctx(A, W, M, N, K, grp, wid0 & 3);
+    const bool g0 = __builtin_amdgcn_readfirstlane(grp) == 0;
+    // DMA pieces of this wave: V2: group-0 wave w moves A pieces {i*4+w} and B pieces {i*4+w}, i < 8;
+    //                          V3: every wave moves A/B pieces {i*8+wid}, i < 4 (as V0).
+    constexpr int NP = SEG32 ? 4 : 8;
+    uint32_t oa[NP], ob[NP];
+    int pa[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int g = SEG32 ? (i * 8 + c.wid) : (i * 4 + (c.wid & 3));
+        pa[i] = g;
+        oa[i] = dma_off(g, c.lane, M - 1 - c.m0, K);
+        ob[i] = dma_off(g, c.lane, N - 1 - c.n0, K);
+    }
+    auto issue = [&](int buf, int kt) {
+        char* na = smem + buf * STB;
+        const uint32_t koff = (uint32_t)kt * (BK * 2);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            dma(c.Ablk, oa[i] + koff, na + pa[i] * 1024);
+            dma(c.Bblk, ob[i] + koff, na + OPB + pa[i] * 1024);
+        }
+    };
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = K / BK;
+    if (SEG32 || g0) issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                   // #0: tile 0 landed for everyone
+    if (!g0) __builtin_amdgcn_s_barrier();         // stagger: group 1 runs one segment behind
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* la = smem + (kt & 1) * STB;
+        const char* lb = la + OPB;
+        const bool pre = kt + 1 < nk;
+        if (!SEG32) {
+            // load segment
+            if (g0 && pre) issue((kt + 1) & 1, kt + 1);
+            bf16x8 a0[8], b0[4], a1[8], b1[4];
+            read_frags(la, lb, 0, c, a0, b0);
+            read_frags(la, lb, 1, c, a1, b1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            // compute segment
+            __builtin_amdgcn_s_setprio(1);
+            mfma32(acc, a0, b0);
+            mfma32(acc, a1, b1);
+            __builtin_amdgcn_s_setprio(0);
+            if (g0 && pre) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                if (ks == 0 && pre) issue((kt + 1) & 1, kt + 1);
+                bf16x8 a[8], b[4];
+                read_frags(la, lb, ks, c, a, b);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                // group 1 retires its DMA at the end of its second load segment; group 0 after its compute
+                if (ks == 1 && pre && !g0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_s_setprio(1);
+                mfma32(acc, a, b);
+                __builtin_amdgcn_s_setprio(0);
+                if (ks == 1 && pre && g0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+            }
+        }
+    }
+    if (g0) __builtin_amdgcn_s_barrier();          // match group 1's extra barrier
+    epilogue(smem, acc, c, bias, C, M, N);
+}
+
+// ---------------------------------------------------------------- host
+static void fill_bf16(std::vector<bf16_t>& v, float scale, unsigned seed) {
+    std::mt19937 g(seed);
+    std::uniform_real_distribution<float> d(-1.f, 1.f);
+    for (auto& x : v) {
+        float f = d(g) * scale;
+        uint32_t u; memcpy(&u, &f, 4);
+        x = (bf16_t)((u + 0x7fff + ((u >> 16) & 1)) >> 16);
+    }
+}
+
+typedef void (*kfn)(const bf16_t*, const bf16_t*, const float*, bf16_t*, int, int, int);
+
+int main(int argc, char** argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 3;
+    struct Shape { const char* name; int M, N, K; };
+    const int Mtok = 4096 * 197;
+    Shape shapes[] = {{"qkv", Mtok, 2304, 768}, {"proj", Mtok, 768, 768}, {"fc1", Mtok, 3072, 768},
+                      {"fc2", Mtok, 768, 3072}};
+    struct Var { const char* name; kfn f; };
+    Var vars[] = {{"V0", k_v01<false>}, {"V1", k_v01<true>}, {"V2", k_pp<false>}, {"V3", k_pp<true>}};
+    const int NV = sizeof(vars) / sizeof(vars[0]);
+    size_t maxA = 0, maxW = 0, maxC = 0;
+    for (auto& s : shapes) {
+        maxA = std::max(maxA, (size_t)s.M * s.K); maxW = std::max(maxW, (size_t)s.N * s.K);
+        maxC = std::max(maxC, (size_t)s.M * s.N);
+    }
+    std::vector<bf16_t> hA(maxA), hW(maxW);
+    fill_bf16(hA, 1.0f, 1); fill_bf16(hW, 0.05f, 2);
+    std::vector<float> hb(4096, 0.01f);
+    bf16_t *dA, *dW, *dC0, *dC;
+    float* db;
+    CHECK(hipMalloc(&dA, maxA * 2)); CHECK(hipMalloc(&dW, maxW * 2));
+    CHECK(hipMalloc(&dC0, maxC * 2)); CHECK(hipMalloc(&dC, maxC * 2)); CHECK(hipMalloc(&db, 4096 * 4));
+    CHECK(hipMemcpy(dA, hA.data(), maxA * 2, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dW, hW.data(), maxW * 2, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(db, hb.data(), 4096 * 4, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+    std::vector<bf16_t> ref(maxC), got(maxC);
+    for (auto& s : shapes) {
+        const int tiles = ((s.M + BM - 1) / BM) * ((s.N + BN - 1) / BN);
+        const double flop = 2.0 * s.M * (double)s.N * s.K;
+        std::vector<std::vector<float>> ms(NV);
+        // correctness vs V0
+        hipLaunchKernelGGL(vars[0].f, dim3(tiles), dim3(512), 0, 0, dA, dW, db, dC0, s.M, s.N, s.K);
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipMemcpy(ref.data(), dC0, (size_t)s.M * s.N * 2, hipMemcpyDeviceToHost));
+        for (int v = 1; v < NV; ++v) {
+            CHECK(hipMemset(dC, 0, (size_t)s.M * s.N * 2));
+            hipLaunchKernelGGL(vars[v].f, dim3(tiles), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipMemcpy(got.data(), dC, (size_t)s.M * s.N * 2, hipMemcpyDeviceToHost));
+            size_t bad = 0;
+            for (size_t i = 0; i < (size_t)s.M * s.N; ++i) bad += got[i] != ref[i];
+            printf("%s %s mismatches vs V0: %zu\n", s.name, vars[v].name, bad);
+        }
+        for (int r = 0; r < rounds; ++r)
+            for (int v = 0; v < NV; ++v) {
+                CHECK(hipEventRecord(e0, 0));
+                for (int it = 0; it < 3; ++it)
+                    hipLaunchKernelGGL(vars[v].f, dim3(tiles), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
+                CHECK(hipEventRecord(e1, 0));
+                CHECK(hipEventSynchronize(e1));
+                float t; CHECK(hipEventElapsedTime(&t, e0, e1));
+                ms[v].push_back(t / 3);
+            }
+        for (int v = 0; v < NV; ++v) {
+            std::sort(ms[v].begin(), ms[v].end());
+            const float med = ms[v][ms[v].size() / 2];
+            printf("%-5s %-3s M=%d N=%d K=%d  median %.3f ms  %.1f TFLOP/s  (min %.3f)\n", s.name, vars[v].name, s.M, s.N,
+                   s.K, med, flop / (med * 1e-3) / 1e12, ms[v][0]);
+        }
+        fflush(stdout);
+    }
+    return 0;
+}
