@@ -263,6 +263,115 @@ __global__ __launch_bounds__(512) void k_pp(const bf16_t* __restrict__ A, const 
     epilogue(smem, acc, c, bias, C, M, N);
 }
 
+
+// ---------------------------------------------------------------- V4 / V5: 32-deep slice ring
+// Ring of R slots, each one 32-deep K-slice of A (256 x 64 B) and B (256 x 64 B) = 32 KiB. 16-B chunk c of row r
+// is stored at c ^ F[(r >> 2) & 3], F = {0, 2, 3, 1} (tools/lds_banks.py: conflict-free fragment reads).
+// V4 (PP = false): all waves in lockstep, one raw barrier per slice, slices issued R-1 ahead, counted vmcnt.
+// V5 (PP = true) : ping-pong groups (waves 4-7 one segment behind); group 0 retires its DMA after its
+//                  compute segment, group 1 after its load segment.
+__device__ __forceinline__ int fsw(int r) { const int g = (r >> 2) & 3; return (((g ^ (g >> 1)) & 1) << 1) | (g >> 1); }
+
+__device__ __forceinline__ uint32_t dma_off32(int g, int lane, int rows_left, int K) {
+    const int row = 16 * g + (lane >> 2);
+    const int lch = (lane & 3) ^ fsw(row);
+    return (uint32_t)min(row, rows_left) * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
+}
+
+__device__ __forceinline__ void read_frags32(const char* la, const char* lb, const Ctx& c, bf16x8 a[8], bf16x8 b[4]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int row = c.wm * 128 + i * 16 + c.fr;
+        a[i] = *reinterpret_cast<const bf16x8*>(la + row * 64 + ((c.fq ^ fsw(row)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = c.wn * 64 + j * 16 + c.fr;
+        b[j] = *reinterpret_cast<const bf16x8*>(lb + row * 64 + ((c.fq ^ fsw(row)) << 4));
+    }
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+__device__ __forceinline__ void wait_vm_rt(int n) {   // n = outstanding slices allowed (0..3)
+    if (n >= 3) wait_vm<12>(); else if (n == 2) wait_vm<8>(); else if (n == 1) wait_vm<4>(); else wait_vm<0>();
+}
+__device__ __forceinline__ void bar() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int R, bool PP>
+__global__ __launch_bounds__(512) void k_ring(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                              const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
+    constexpr int SLOT = 32768;
+    __shared__ __attribute__((aligned(16))) char smem[R * SLOT];
+    const int wid0 = threadIdx.x >> 6;
+    const int grp = wid0 >> 2;
+    Ctx c = make_ctx(A, W, M, N, K, grp, wid0 & 3);
+    const bool g1 = PP && __builtin_amdgcn_readfirstlane(grp) == 1;
+    uint32_t oa[2], ob[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        oa[i] = dma_off32(i * 8 + c.wid, c.lane, M - 1 - c.m0, K);
+        ob[i] = dma_off32(i * 8 + c.wid, c.lane, N - 1 - c.n0, K);
+    }
+    auto issue = [&](int slot, int sl) {
+        char* d = smem + slot * SLOT;
+        const uint32_t koff = (uint32_t)sl * 64;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            dma(c.Ablk, oa[i] + koff, d + (i * 8 + c.wid) * 1024);
+            dma(c.Bblk, ob[i] + koff, d + 16384 + (i * 8 + c.wid) * 1024);
+        }
+    };
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int ns = K / 32;
+    for (int sl = 0; sl < R - 1 && sl < ns; ++sl) issue(sl, sl);
+    if (!PP) {
+        for (int sl = 0; sl < ns; ++sl) {
+            wait_vm_rt(min(R - 2, ns - 1 - sl));
+            bar();
+            if (sl + R - 1 < ns) issue((sl + R - 1) % R, sl + R - 1);
+            const char* la = smem + (sl % R) * SLOT;
+            bf16x8 a[8], b[4];
+            read_frags32(la, la + 16384, c, a, b);
+            mfma32(acc, a, b);
+        }
+    } else {
+        wait_vm_rt(min(R - 2, ns - 1));            // slice 0 of every wave
+        bar();                                      // #0
+        if (g1) bar();                              // stagger
+        for (int sl = 0; sl < ns; ++sl) {
+            // load segment
+            if (sl + R - 1 < ns) issue((sl + R - 1) % R, sl + R - 1);
+            const char* la = smem + (sl % R) * SLOT;
+            bf16x8 a[8], b[4];
+            read_frags32(la, la + 16384, c, a, b);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (g1 && sl + 1 < ns) wait_vm_rt(min(R - 2, ns - 2 - sl));   // my share of slice sl+1
+            bar();
+            __builtin_amdgcn_s_setprio(1);
+            mfma32(acc, a, b);
+            __builtin_amdgcn_s_setprio(0);
+            if (!g1 && sl + 1 < ns) wait_vm_rt(min(R - 2, ns - 2 - sl));
+            bar();
+        }
+        if (!g1) bar();
+    }
+    epilogue(smem, acc, c, bias, C, M, N);
+}
+
 // ---------------------------------------------------------------- host
 static void fill_bf16(std::vector<bf16_t>& v, float scale, unsigned seed) {
     std::mt19937 g(seed);
@@ -278,12 +387,17 @@ typedef void (*kfn)(const bf16_t*, const bf16_t*, const float*, bf16_t*, int, in
 
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 3;
+    const char* shape_filter = argc > 2 ? argv[2] : "";      // e.g. "fc2"
+    const char* var_filter = argc > 3 ? argv[3] : "";        // e.g. "V0,V3"
+    const bool check = argc <= 4 || atoi(argv[4]) != 0;
     struct Shape { const char* name; int M, N, K; };
     const int Mtok = 4096 * 197;
     Shape shapes[] = {{"qkv", Mtok, 2304, 768}, {"proj", Mtok, 768, 768}, {"fc1", Mtok, 3072, 768},
                       {"fc2", Mtok, 768, 3072}};
     struct Var { const char* name; kfn f; };
-    Var vars[] = {{"V0", k_v01<false>}, {"V1", k_v01<true>}, {"V2", k_pp<false>}, {"V3", k_pp<true>}};
+    Var vars[] = {{"V0", k_v01<false>}, {"V1", k_v01<true>}, {"V2", k_pp<false>}, {"V3", k_pp<true>},
+                  {"V4r4", k_ring<4, false>}, {"V4r5", k_ring<5, false>}, {"V5r4", k_ring<4, true>},
+                  {"V5r5", k_ring<5, true>}};
     const int NV = sizeof(vars) / sizeof(vars[0]);
     size_t maxA = 0, maxW = 0, maxC = 0;
     for (auto& s : shapes) {
@@ -304,9 +418,12 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
     std::vector<bf16_t> ref(maxC), got(maxC);
     for (auto& s : shapes) {
+        if (shape_filter[0] && !strstr(shape_filter, s.name)) continue;
         const int tiles = ((s.M + BM - 1) / BM) * ((s.N + BN - 1) / BN);
         const double flop = 2.0 * s.M * (double)s.N * s.K;
         std::vector<std::vector<float>> ms(NV);
+        auto on = [&](int v) { return !var_filter[0] || strstr(var_filter, vars[v].name); };
+        if (check) {
         // correctness vs V0
         hipLaunchKernelGGL(vars[0].f, dim3(tiles), dim3(512), 0, 0, dA, dW, db, dC0, s.M, s.N, s.K);
         CHECK(hipDeviceSynchronize());
@@ -320,8 +437,10 @@ int main(int argc, char** argv) {
             for (size_t i = 0; i < (size_t)s.M * s.N; ++i) bad += got[i] != ref[i];
             printf("%s %s mismatches vs V0: %zu\n", s.name, vars[v].name, bad);
         }
+        }
         for (int r = 0; r < rounds; ++r)
             for (int v = 0; v < NV; ++v) {
+                if (!on(v)) { ms[v].push_back(0.f); continue; }
                 CHECK(hipEventRecord(e0, 0));
                 for (int it = 0; it < 3; ++it)
                     hipLaunchKernelGGL(vars[v].f, dim3(tiles), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);

@@ -45,3 +45,11 @@ for it in range(16):
         addr.append(m*128 + ((c16 ^ (esw(m) >> 1)) * 16))
     worst = max(worst, cycles_read128(addr))
 print("epilogue ds_read_b128 worst cycles (4=free):", worst)
+# 64-B rows (BK = 32 ring): 16-B chunk c of row r at c ^ f(r), f(r) = F[(r >> 2) & 3]
+F = [0, 2, 3, 1]
+f64 = lambda r: F[(r >> 2) & 3]
+worst = 0
+for base in range(0, 256, 16):
+    addr = [(base + (l & 15)) * 64 + (((l >> 4) ^ f64(base + (l & 15))) * 16) for l in range(64)]
+    worst = max(worst, cycles_read128(addr))
+print("BK32 operand ds_read_b128 worst cycles (4=free):", worst)

@@ -39,10 +39,82 @@ __device__ __forceinline__ bf16x4 ds_read_tr(const char* lds_base, int byte_off)
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_v4*>(p));
 }
 
-__global__ __launch_bounds__(256) void k_attn_bf16(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+// One key step of T 32-key tiles (T = 1 or 2) for a 32-query strip: S^T = K Q^T on MFMA, online softmax
+// update of (m, l, O), O^T += V^T P^T with V^T fragments from transposed LDS reads.
+template <int T>
+__device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb, int N, int lane, const bf16x8 qf[4],
+                                          float scale_log2, float& m, float& l, f32x16& o0, f32x16& o1) {
+    const int l32 = lane & 31, hh = lane >> 5;
+    f32x16 s[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        s[t] = f32x16{};
+        const int kr = kb + t * 32 + l32;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
+            s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[t], 0, 0, 0);
+        }
+    }
+    float bm = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = kb + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const float v = key < N ? s[t][r] : -INFINITY;
+            s[t][r] = v;
+            bm = fmaxf(bm, v);
+        }
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+    m = mn;
+    const float msc = mn * scale_log2;
+    l *= alpha;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    bf16x8 pf[T][2];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[t][r], scale_log2, -msc));
+            s[t][r] = p;
+            l += p;
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            const uint4 u = make_uint4(pack_bf2(s[t][8 * st + 0], s[t][8 * st + 1]), pack_bf2(s[t][8 * st + 2], s[t][8 * st + 3]),
+                                       pack_bf2(s[t][8 * st + 4], s[t][8 * st + 5]), pack_bf2(s[t][8 * st + 6], s[t][8 * st + 7]));
+            pf[t][st] = __builtin_bit_cast(bf16x8, u);
+        }
+    }
+    const int grp = lane >> 4, gi = lane & 15;
+    const int rq = gi >> 2, cp = gi & 3;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            const int rbase = kb + t * 32 + st * 16 + 4 * (grp >> 1) + rq;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
+                const int c16 = col >> 3, inner = (col & 7) * 2;
+                const bf16x4 lo = ds_read_tr(Vs, v_off(rbase, c16) + inner);
+                const bf16x4 hi = ds_read_tr(Vs, v_off(rbase + 8, c16) + inner);
+                const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][st], o0, 0, 0, 0);
+                else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][st], o1, 0, 0, 0);
+            }
+        }
+}
+
+// One workgroup per (particle, head); one wave per 32-query strip (up to 8 waves, strips beyond loop).
+__global__ __launch_bounds__(512) void k_attn_bf16(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                    int N, int H, float scale_log2, int q_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int NP = (N + 63) & ~63;
+    const int NP = (N + 31) & ~31;       // keys padded to whole 32-key MFMA tiles
     char* Ks = smem;
     char* Vs = smem + NP * ROWB;
     const int bh = blockIdx.x;
@@ -52,10 +124,9 @@ __global__ __launch_bounds__(256) void k_attn_bf16(const bf16_t* __restrict__ qk
     const bf16_t* qbase = qkv + row0 * 3 * D + h * HD;
     const bf16_t* kbase = qbase + D;
     const bf16_t* vbase = qbase + 2 * D;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
 
-    // ---- stage K and V (16-B chunks, 8 per row) ----
-    for (int idx = tid; idx < NP * 8; idx += 256) {
+    for (int idx = tid; idx < NP * 8; idx += blockDim.x) {
         const int r = idx >> 3, c = idx & 7;
         uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
         if (r < N) {
@@ -69,9 +140,8 @@ __global__ __launch_bounds__(256) void k_attn_bf16(const bf16_t* __restrict__ qk
 
     const int l32 = lane & 31, hh = lane >> 5;
     const int nstrips = (q_rows + 31) >> 5;
-    for (int strip = wid; strip < nstrips; strip += 4) {
+    for (int strip = wid; strip < nstrips; strip += nw) {
         const int q = strip * 32 + l32;
-        // Q^T fragments (B operand): lane holds Q[q][16ks + 8hh + j]
         bf16x8 qf[4];
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
@@ -80,76 +150,9 @@ __global__ __launch_bounds__(256) void k_attn_bf16(const bf16_t* __restrict__ qk
         }
         f32x16 o0 = {}, o1 = {};
         float m = -INFINITY, l = 0.f;
-        for (int kb = 0; kb < NP; kb += 64) {
-            f32x16 s[2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                s[t] = f32x16{};
-                const int kr = kb + t * 32 + l32;   // key row this lane supplies for the A operand
-#pragma unroll
-                for (int ks = 0; ks < 4; ++ks) {
-                    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
-                    s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[t], 0, 0, 0);
-                }
-            }
-            // mask padded keys, block max
-            float bm = -INFINITY;
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = kb + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                    const float v = key < N ? s[t][r] : -INFINITY;
-                    s[t][r] = v;
-                    bm = fmaxf(bm, v);
-                }
-            bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-            const float mn = fmaxf(m, bm);
-            const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
-            m = mn;
-            const float msc = mn * scale_log2;
-            l *= alpha;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-            bf16x8 pf[2][2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float p = __builtin_amdgcn_exp2f(fmaf(s[t][r], scale_log2, -msc));
-                    s[t][r] = p;
-                    l += p;
-                }
-#pragma unroll
-                for (int st = 0; st < 2; ++st) {
-                    uint32_t w0 = pack_bf2(s[t][8 * st + 0], s[t][8 * st + 1]);
-                    uint32_t w1 = pack_bf2(s[t][8 * st + 2], s[t][8 * st + 3]);
-                    uint32_t w2 = pack_bf2(s[t][8 * st + 4], s[t][8 * st + 5]);
-                    uint32_t w3 = pack_bf2(s[t][8 * st + 6], s[t][8 * st + 7]);
-                    const uint4 u = make_uint4(w0, w1, w2, w3);
-                    pf[t][st] = __builtin_bit_cast(bf16x8, u);
-                }
-            }
-            // O^T[d][q] += V^T[d][key] P^T[key][q]; A fragments by transposed LDS reads
-            const int grp = lane >> 4, gi = lane & 15;
-            const int rq = gi >> 2, cp = gi & 3;
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int st = 0; st < 2; ++st) {
-                    const int rbase = kb + t * 32 + st * 16 + 4 * (grp >> 1) + rq;
-#pragma unroll
-                    for (int dt = 0; dt < 2; ++dt) {
-                        const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;   // element column
-                        const int c16 = col >> 3, inner = (col & 7) * 2;
-                        const bf16x4 lo = ds_read_tr(Vs, v_off(rbase, c16) + inner);
-                        const bf16x4 hi = ds_read_tr(Vs, v_off(rbase + 8, c16) + inner);
-                        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                        if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][st], o0, 0, 0, 0);
-                        else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][st], o1, 0, 0, 0);
-                    }
-                }
-        }
+        int kb = 0;
+        for (; kb + 64 <= NP; kb += 64) attn_step<2>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+        if (kb < NP) attn_step<1>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
         l += __shfl_xor(l, 32, 64);
         const float inv = 1.0f / l;
         if (q < q_rows) {
@@ -214,16 +217,18 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     if (B < 0 || N <= 0 || N > 640 || H <= 0 || hd != HD || B * H > INT32_MAX || q_rows < 1 || q_rows > N)
         return VPF_ERR_ARG;
     if (B == 0) return 0;
-    const int NP = (N + 63) & ~63;
+    const int NP = (N + 31) & ~31;
     const size_t lds = (size_t)NP * ROWB * 2;
     const float scale_log2 = scale * 1.44269504088896341f;
+    const int strips = (q_rows + 31) / 32;
+    const int threads = 64 * (strips < 8 ? strips : 8);
     static bool attr_set = false;   // benign race: idempotent attribute set
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_attn_bf16, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    hipLaunchKernelGGL(k_attn_bf16, dim3((unsigned)(B * H)), dim3(256), lds, (hipStream_t)stream, qkv, out, N, H,
-                       scale_log2, q_rows);
+    hipLaunchKernelGGL(k_attn_bf16, dim3((unsigned)(B * H)), dim3(threads), lds, (hipStream_t)stream, qkv, out, N,
+                       H, scale_log2, q_rows);
     VPF_RETURN_LAUNCH();
 }
 

@@ -37,24 +37,25 @@ constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KiB
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
-__device__ __forceinline__ float gelu_erf(float x) {
-    // x * Phi(x) with erfc from Numerical Recipes' erfcc (|relative error| < 1.2e-7 everywhere).
-    const float z = fabsf(x) * 0.70710678118654752f;
-    const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
-    float p = 0.17087277f;
-    p = fmaf(p, t, -0.82215223f);
-    p = fmaf(p, t, 1.48851587f);
-    p = fmaf(p, t, -1.13520398f);
-    p = fmaf(p, t, 0.27886807f);
-    p = fmaf(p, t, -0.18628806f);
-    p = fmaf(p, t, 0.09678418f);
-    p = fmaf(p, t, 0.37409196f);
-    p = fmaf(p, t, 1.00002368f);
-    p = fmaf(p, t, -1.26551223f);
-    const float e = fmaf(-z, z, p);
-    const float half_erfc = 0.5f * t * __builtin_amdgcn_exp2f(e * 1.44269504088896341f);
-    const float phi = x >= 0.0f ? 1.0f - half_erfc : half_erfc;
-    return x * phi;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Exact-erf GELU, two lanes' worth at a time so the polynomial runs on packed FP32 (v_pk_fma_f32):
+// x * Phi(x), Phi(x) = 0.5 + 0.5 sign(x) erf(|x|/sqrt2), erf(z) = 1 - t(a1 + t(a2 + t(a3 + t(a4 + t a5)))) e^{-z^2},
+// t = 1/(1 + p z) (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7: below bf16 resolution by > 10^4).
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+    const f32x2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+    const f32x2 den = z * 0.3275911f + 1.0f;
+    const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    f32x2 p = t * 1.061405429f - 1.453152027f;
+    p = p * t + 1.421413741f;
+    p = p * t - 0.284496736f;
+    p = p * t + 0.254829592f;
+    p = p * t;
+    const f32x2 ez = z * z * -1.44269504088896341f;
+    const f32x2 e = {__builtin_amdgcn_exp2f(ez.x), __builtin_amdgcn_exp2f(ez.y)};
+    const f32x2 erf_abs = 1.0f - p * e;
+    const f32x2 half = {__builtin_copysignf(0.5f, x.x), __builtin_copysignf(0.5f, x.y)};
+    return x * (half * erf_abs + 0.5f);
 }
 
 template <int EPI>
@@ -114,6 +115,26 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
 
     // fragment read addresses (byte offsets inside an operand tile), excluding the ks chunk term
     const int fr = lane & 15, fq = lane >> 4;
+
+    // Epilogue operands are loaded before the K loop so their latency hides under it: bias (and, for the
+    // folded LayerNorm, colsum and the per-row statistics) in the accumulator layout of this lane.
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    float4 bv[4], cv[4];
+    float2 rs[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ng = n0 + wn * 64 + j * 16 + fq * 4;
+        bv[j] = ng < N ? *reinterpret_cast<const float4*>(bias + ng) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (LN) cv[j] = ng < N ? *reinterpret_cast<const float4*>(colsum + ng) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if constexpr (LN) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int m = m0 + wm * 128 + i * 16 + fr;
+            const float2 st = m < M ? stats[m] : make_float2(0.f, 0.f);
+            rs[i] = make_float2(st.y, -st.y * st.x);   // (rstd, -rstd * mean)
+        }
+    }
     const int nk = K / BK;
     stage(0, 0);
     for (int kt = 0; kt < nk; ++kt) {
@@ -147,47 +168,44 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     // ---------------- epilogue ----------------
     __syncthreads();   // every wave is done with the operand ring; reuse it as 8 x 16 KiB images
     char* img = smem + wid * 16384;
-    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
-    float2 rs[8];   // LN-fold: per-row (rstd, -rstd*mean) of this lane's 8 rows
-    if constexpr (LN) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int m = m0 + wm * 128 + i * 16 + fr;
-            const float2 st = m < M ? stats[m] : make_float2(0.f, 0.f);
-            rs[i] = make_float2(st.y, -st.y * st.x);
-        }
-    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int nl = wn * 64 + j * 16 + fq * 4;     // column (within the block tile) of this lane's 4 values
-        const int ng = n0 + nl;
-        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f), cv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
-        if constexpr (LN) { if (ng < N) cv = *reinterpret_cast<const float4*>(colsum + ng); }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             float v0, v1, v2, v3;
             if constexpr (LN) {
                 // LN(x) W^T + b = rstd (x W'^T) - rstd mean colsum(W') + b'   (gamma folded into W', beta into b')
-                v0 = fmaf(rs[i].x, acc[j][i][0], fmaf(rs[i].y, cv.x, bv.x));
-                v1 = fmaf(rs[i].x, acc[j][i][1], fmaf(rs[i].y, cv.y, bv.y));
-                v2 = fmaf(rs[i].x, acc[j][i][2], fmaf(rs[i].y, cv.z, bv.z));
-                v3 = fmaf(rs[i].x, acc[j][i][3], fmaf(rs[i].y, cv.w, bv.w));
+                v0 = fmaf(rs[i].x, acc[j][i][0], fmaf(rs[i].y, cv[j].x, bv[j].x));
+                v1 = fmaf(rs[i].x, acc[j][i][1], fmaf(rs[i].y, cv[j].y, bv[j].y));
+                v2 = fmaf(rs[i].x, acc[j][i][2], fmaf(rs[i].y, cv[j].z, bv[j].z));
+                v3 = fmaf(rs[i].x, acc[j][i][3], fmaf(rs[i].y, cv[j].w, bv[j].w));
             } else {
-                v0 = acc[j][i][0] + bv.x; v1 = acc[j][i][1] + bv.y;
-                v2 = acc[j][i][2] + bv.z; v3 = acc[j][i][3] + bv.w;
+                v0 = acc[j][i][0] + bv[j].x; v1 = acc[j][i][1] + bv[j].y;
+                v2 = acc[j][i][2] + bv[j].z; v3 = acc[j][i][3] + bv[j].w;
             }
             if constexpr (EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU) {
-                v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+                const f32x2 g01 = gelu_erf2(f32x2{v0, v1}), g23 = gelu_erf2(f32x2{v2, v3});
+                v0 = g01.x; v1 = g01.y; v2 = g23.x; v3 = g23.y;
             }
             const int row = i * 16 + fr;              // row within the wave's 128-row image
             const int c8 = (j * 4 + fq) ^ (row & 15);  // swizzled 8-B chunk
             *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
         }
     }
-    __syncthreads();
     const int c16 = lane & 7;
-#pragma unroll 4
+    uint4 res[16];
+    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
+        // all 16 residual rows of this lane in flight at once, under the LDS round trip below
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int m = m0 + wm * 128 + it * 8 + (lane >> 3);
+            const int n = n0 + wn * 64 + c16 * 8;
+            res[it] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(residual + (int64_t)m * ldc + n)
+                                       : make_uint4(0, 0, 0, 0);
+        }
+    }
+    __syncthreads();
+#pragma unroll
     for (int it = 0; it < 16; ++it) {
         const int row = it * 8 + (lane >> 3);
         uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
@@ -211,7 +229,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             v = make_uint4(o[0], o[1], o[2], o[3]);
         }
         if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
-            const uint4 rv = *reinterpret_cast<const uint4*>(residual + (int64_t)m * ldc + n);
+            const uint4 rv = res[it];
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
             const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
             uint32_t o[4];
