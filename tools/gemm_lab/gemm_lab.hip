@@ -66,7 +66,20 @@ __device__ __forceinline__ void dma(const char* base, uint32_t off, char* lds) {
     __builtin_amdgcn_global_load_lds((gptr_t)(base + off), (lptr_t)lds, 16, 0, 0);
 }
 
+#ifndef LAB_IMM
+#define LAB_IMM 1
+#endif
 __device__ __forceinline__ void read_frags(const char* la, const char* lb, int ks, const Ctx& c, bf16x8 a[8], bf16x8 b[4]) {
+#if LAB_IMM
+    // rows i*16 + fr share the swizzle term ((fr >> 1) & 7): one base address + i * 2048 immediates
+    const int sw = (c.fr >> 1) & 7;
+    const char* pa = la + (c.wm * 128 + c.fr) * 128 + (((ks * 4 + c.fq) ^ sw) << 4);
+    const char* pb = lb + (c.wn * 64 + c.fr) * 128 + (((ks * 4 + c.fq) ^ sw) << 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(pa + i * 2048);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(pb + j * 2048);
+#else
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int row = c.wm * 128 + i * 16 + c.fr;
@@ -77,6 +90,7 @@ __device__ __forceinline__ void read_frags(const char* la, const char* lb, int k
         const int row = c.wn * 64 + j * 16 + c.fr;
         b[j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + (((ks * 4 + c.fq) ^ ((row >> 1) & 7)) << 4));
     }
+#endif
 }
 
 __device__ __forceinline__ void mfma32(f32x4 acc[4][8], const bf16x8 a[8], const bf16x8 b[4]) {
@@ -117,7 +131,7 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 acc[4][8], const Ctx&
 }
 
 // ---------------------------------------------------------------- V0 / V1
-template <bool SPREAD>
+template <bool SPREAD, bool SAMEK = false>
 __global__ __launch_bounds__(512) void k_v01(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                              const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
     __shared__ __attribute__((aligned(16))) char smem[LDSB];
@@ -145,7 +159,7 @@ __global__ __launch_bounds__(512) void k_v01(const bf16_t* __restrict__ A, const
         const char* la = smem + (kt & 1) * STB;
         const char* lb = la + OPB;
         char* na = smem + ((kt + 1) & 1) * STB;
-        const uint32_t koff = (uint32_t)(kt + 1) * (BK * 2);
+        const uint32_t koff = SAMEK ? 0u : (uint32_t)(kt + 1) * (BK * 2);   // SAMEK: timing probe only
         const bool pre = kt + 1 < nk;
         if (!SPREAD && pre) {
 #pragma unroll
@@ -372,6 +386,685 @@ __global__ __launch_bounds__(512) void k_ring(const bf16_t* __restrict__ A, cons
     epilogue(smem, acc, c, bias, C, M, N);
 }
 
+
+
+// ---------------------------------------------------------------- V7: ping-pong + DMA inside compute segments
+// Two groups (waves 0-3 / 4-7, one of each per SIMD) one segment apart; segments are 32-deep (12 ds_read_b128
+// load segment / 32 MFMA compute segment). Each wave's 8 DMA pieces of a K-tile are issued INSIDE a compute
+// segment, one per 4 MFMAs, so the address/TA path streams while the matrix pipe runs:
+//   group 0 issues tile k+1 in its first compute segment of tile k, retires it (vmcnt 0) after its second;
+//   group 1 issues tile k+1 in its second compute segment of tile k-1, retires it after its second load
+//   segment of tile k. Both writes land in the buffer of tile k-1 after every read of it (WAR) and before
+//   the first read of tile k+1 (RAW: a barrier separates the retiring wait and the first reader).
+template <bool PRIO>
+__global__ __launch_bounds__(512) void k_v7(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                            const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[LDSB];
+    const int wid0 = threadIdx.x >> 6;
+    const int grp = wid0 >> 2;
+    Ctx c = make_ctx(A, W, M, N, K, grp, wid0 & 3);
+    const bool g1 = __builtin_amdgcn_readfirstlane(grp) == 1;
+    uint32_t oa[4], ob[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        oa[i] = dma_off(i * 8 + c.wid, c.lane, M - 1 - c.m0, K);
+        ob[i] = dma_off(i * 8 + c.wid, c.lane, N - 1 - c.n0, K);
+    }
+    auto issue_piece = [&](int buf, int kt, int p) {   // p in [0, 8): A pieces 0..3, B pieces 4..7
+        char* na = smem + buf * STB;
+        const uint32_t koff = (uint32_t)kt * (BK * 2);
+        if (p < 4) dma(c.Ablk, oa[p] + koff, na + (p * 8 + c.wid) * 1024);
+        else dma(c.Bblk, ob[p - 4] + koff, na + OPB + ((p - 4) * 8 + c.wid) * 1024);
+    };
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = K / BK;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) issue_piece(0, 0, p);
+    if (g1 && nk > 1) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) issue_piece(1, 1, p);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();                                          // #0: tile 0 landed
+    if (g1) bar();                                  // stagger
+    if (PRIO && g1) __builtin_amdgcn_s_setprio(1);
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* la = smem + (kt & 1) * STB;
+        const char* lb = la + OPB;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            // ---- load segment
+            bf16x8 a[8], b[4];
+            read_frags(la, lb, ks, c, a, b);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (g1 && ks == 1 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // my share of tile kt+1
+            bar();
+            // ---- compute segment (+ DMA pieces)
+            const int dt = g1 ? kt + 2 : kt + 1;          // tile whose pieces this wave streams now
+            const bool dma_now = (g1 ? ks == 1 : ks == 0) && dt < nk;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
+                    if ((i & 3) == 3 && dma_now) issue_piece(dt & 1, dt, j * 2 + (i >> 2));
+                }
+            }
+            if (!g1 && ks == 1 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();
+        }
+    }
+    if (PRIO && g1) __builtin_amdgcn_s_setprio(0);
+    if (!g1) bar();
+    epilogue(smem, acc, c, bias, C, M, N);
+}
+
+
+// ---------------------------------------------------------------- V8: V0 structure on v_mfma_f32_32x32x16_bf16
+// Wave tile 128 (m) x 64 (n) = 4 x 2 tiles of 32 x 32 (8 x 16 accumulator VGPRs). Swapped operands: the W
+// fragment is the A operand, so D[n][m] has m on the lane and 4 consecutive n per register group.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(512) void k_v8(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                            const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[LDSB];
+    const int wid0 = threadIdx.x >> 6;
+    Ctx c = make_ctx(A, W, M, N, K, wid0 >> 2, wid0 & 3);
+    const int l32 = c.lane & 31, hh = c.lane >> 5;
+    uint32_t oa[4], ob[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        oa[i] = dma_off(i * 8 + c.wid, c.lane, M - 1 - c.m0, K);
+        ob[i] = dma_off(i * 8 + c.wid, c.lane, N - 1 - c.n0, K);
+    }
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][i] = f32x16{};
+    const int nk = K / BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        dma(c.Ablk, oa[i], smem + (i * 8 + c.wid) * 1024);
+        dma(c.Bblk, ob[i], smem + OPB + (i * 8 + c.wid) * 1024);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();
+        const char* la = smem + (kt & 1) * STB;
+        const char* lb = la + OPB;
+        char* na = smem + ((kt + 1) & 1) * STB;
+        const uint32_t koff = (uint32_t)(kt + 1) * (BK * 2);
+        if (kt + 1 < nk) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                dma(c.Ablk, oa[i] + koff, na + (i * 8 + c.wid) * 1024);
+                dma(c.Bblk, ob[i] + koff, na + OPB + (i * 8 + c.wid) * 1024);
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            bf16x8 a[4], b[2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = c.wm * 128 + i * 32 + l32;
+                a[i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + (((kk * 2 + hh) ^ ((row >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = c.wn * 64 + j * 32 + l32;
+                b[j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + (((kk * 2 + hh) ^ ((row >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    char* img = smem + c.wid * 16384;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int ng = c.n0 + c.wn * 64 + j * 32 + 8 * g + 4 * hh;
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = i * 32 + l32;
+                const int c8 = (j * 8 + 2 * g + hh) ^ (row & 15);
+                *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
+                    make_uint2(pack_bf2(acc[j][i][4 * g] + bv.x, acc[j][i][4 * g + 1] + bv.y),
+                               pack_bf2(acc[j][i][4 * g + 2] + bv.z, acc[j][i][4 * g + 3] + bv.w));
+            }
+        }
+    __builtin_amdgcn_wave_barrier();
+    const int c16 = c.lane & 7;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+        const int row = it * 8 + (c.lane >> 3);
+        uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+        if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+        const int m = c.m0 + c.wm * 128 + row, n = c.n0 + c.wn * 64 + c16 * 8;
+        if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * N + n) = v;
+    }
+}
+
+
+// ---------------------------------------------------------------- V9: wave-specialised producer / consumer
+// Block tile 256 (m) x 128 (n), BK = 64, 3-stage LDS ring (48 KiB per stage: A 256 rows + B 128 rows).
+// Waves 0-3 (one per SIMD) only read LDS and issue MFMAs (wave tile 128 x 64, 128 accumulators, fragments
+// double-buffered across the two 32-deep halves of a stage); waves 4-7 only issue LDS-DMA (12 pieces per
+// stage each) and retire it with a counted vmcnt. One barrier per K-step: at barrier s, stage s has landed
+// (loaders waited before arriving) and stage s-1's slot is free (consumers finished reading it).
+constexpr int V9_STAGE = 256 * 128 + 128 * 128;   // 48 KiB
+__global__ __launch_bounds__(512) void k_v9(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                            const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * V9_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool loader = wid >= 4;
+    // tile mapping (XCD-aware), BN = 128
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tiles_n = (N + 127) / 128;
+    const int tm = lid / tiles_n, tn = lid - tm * tiles_n;
+    const int m0 = tm * 256, n0 = tn * 128;
+    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * K * 2;
+    const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2;
+    const int nk = K / 64;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int wm = (wid & 3) >> 1, wn = wid & 1;
+
+    if (loader) {
+        const int lw = wid - 4;
+        uint32_t oa[8], ob[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) oa[i] = dma_off(i * 4 + lw, lane, M - 1 - m0, K);    // A pieces g = i*4 + lw (32)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ob[i] = dma_off(i * 4 + lw, lane, N - 1 - n0, K);    // B pieces (16)
+        auto issue = [&](int st) {
+            char* d = smem + (st % 3) * V9_STAGE;
+            const uint32_t koff = (uint32_t)st * 128;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dma(Ablk, oa[i] + koff, d + (i * 4 + lw) * 1024);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dma(Bblk, ob[i] + koff, d + 32768 + (i * 4 + lw) * 1024);
+        };
+        issue(0);
+        if (nk > 1) issue(1);
+        if (nk > 1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();                                      // B_0: stage 0 landed
+        for (int st = 0; st < nk; ++st) {
+            if (st + 2 < nk) issue(st + 2);         // slot of stage st-1: free since B_st
+            if (st + 1 < nk) {
+                if (st + 2 < nk) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                bar();                              // B_{st+1}: stage st+1 landed
+            }
+        }
+        bar();                                      // epilogue barrier (matches consumers)
+        return;
+    }
+    // ---------------- consumers
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bar();                                          // B_0
+    for (int st = 0; st < nk; ++st) {
+        const char* la = smem + (st % 3) * V9_STAGE;
+        const char* lb = la + 32768;
+        bf16x8 a0[8], b0[4], a1[8], b1[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = wm * 128 + i * 16 + fr;
+            a0[i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + (((0 + fq) ^ ((row >> 1) & 7)) << 4));
+            a1[i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + (((4 + fq) ^ ((row >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = wn * 64 + j * 16 + fr;
+            b0[j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + (((0 + fq) ^ ((row >> 1) & 7)) << 4));
+            b1[j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + (((4 + fq) ^ ((row >> 1) & 7)) << 4));
+        }
+        mfma32(acc, a0, b0);
+        mfma32(acc, a1, b1);
+        if (st + 1 < nk) bar();                     // B_{st+1}
+    }
+    // epilogue (consumers only; loaders wait at the matching barrier so the ring is free)
+    bar();
+    char* img = smem + wid * 16384;
+    {
+        Ctx c; c.m0 = m0; c.n0 = n0; c.wid = wid; c.lane = lane; c.wm = wm; c.wn = wn; c.fr = fr; c.fq = fq;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ng = n0 + wn * 64 + j * 16 + fq * 4;
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = i * 16 + fr;
+                const int c8 = (j * 4 + fq) ^ (row & 15);
+                *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
+                    make_uint2(pack_bf2(acc[j][i][0] + bv.x, acc[j][i][1] + bv.y), pack_bf2(acc[j][i][2] + bv.z, acc[j][i][3] + bv.w));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int c16 = lane & 7;
+#pragma unroll 4
+        for (int it = 0; it < 16; ++it) {
+            const int row = it * 8 + (lane >> 3);
+            uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+            if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+            const int m = m0 + wm * 128 + row, n = n0 + wn * 64 + c16 * 8;
+            if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * N + n) = v;
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------- V10: V9 with a mid-stage barrier
+// Consumers hold the first-half (k 0-31) fragments of stage s in registers when stage s starts; they issue
+// the second-half reads, run the first-half MFMAs, pass barrier X_s (loaders guarantee stage s+1 landed),
+// issue stage s+1's first-half reads and run stage s's second-half MFMAs: every LDS read is covered by 32
+// MFMAs. A slot is free after X_s for the stage it held (both halves were read between X_{s-1} and X_s).
+__global__ __launch_bounds__(512) void k_v10(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                             const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * V9_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool loader = wid >= 4;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tiles_n = (N + 127) / 128;
+    const int tm = lid / tiles_n, tn = lid - tm * tiles_n;
+    const int m0 = tm * 256, n0 = tn * 128;
+    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * K * 2;
+    const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2;
+    const int nk = K / 64;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int wm = (wid & 3) >> 1, wn = wid & 1;
+
+    if (loader) {
+        const int lw = wid - 4;
+        uint32_t oa[8], ob[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) oa[i] = dma_off(i * 4 + lw, lane, M - 1 - m0, K);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ob[i] = dma_off(i * 4 + lw, lane, N - 1 - n0, K);
+        auto issue = [&](int st) {
+            char* d = smem + (st % 3) * V9_STAGE;
+            const uint32_t koff = (uint32_t)st * 128;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dma(Ablk, oa[i] + koff, d + (i * 4 + lw) * 1024);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dma(Bblk, ob[i] + koff, d + 32768 + (i * 4 + lw) * 1024);
+        };
+        issue(0);
+        if (nk > 1) issue(1);
+        if (nk > 1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();                                      // X_-1: stage 0 landed
+        for (int st = 0; st + 1 < nk; ++st) {
+            // after X_{st-1}: the slot of stage st-1 is free -> stage st+2 (issued for st >= 1; st+2 < nk)
+            if (st + 2 < nk) issue(st + 2);      // slot (st+2)%3 held stage st-1 (or is unused for st = 0)
+            // X_st must certify stage st+1
+            if (st + 2 < nk) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();                                  // X_st
+        }
+        bar();                                      // epilogue
+        return;
+    }
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int sw = (fr >> 1) & 7;
+    const int aoff0 = (wm * 128 + fr) * 128 + ((fq ^ sw) << 4), aoff1 = (wm * 128 + fr) * 128 + (((4 + fq) ^ sw) << 4);
+    const int boff0 = 32768 + (wn * 64 + fr) * 128 + ((fq ^ sw) << 4), boff1 = 32768 + (wn * 64 + fr) * 128 + (((4 + fq) ^ sw) << 4);
+    auto rd = [&](const char* la, int half, bf16x8 a[8], bf16x8 b[4]) {
+        const char* pa = la + (half ? aoff1 : aoff0);
+        const char* pb = la + (half ? boff1 : boff0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(pa + i * 2048);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(pb + j * 2048);
+    };
+    bar();                                          // X_-1
+    bf16x8 a0[8], b0[4], a1[8], b1[4];
+    rd(smem, 0, a0, b0);
+    for (int st = 0; st < nk; ++st) {
+        const char* la = smem + (st % 3) * V9_STAGE;
+        rd(la, 1, a1, b1);
+        mfma32(acc, a0, b0);
+        if (st + 1 < nk) {
+            bar();                                  // X_st: stage st+1 landed; stage st-1's slot free
+            rd(smem + ((st + 1) % 3) * V9_STAGE, 0, a0, b0);
+        }
+        mfma32(acc, a1, b1);
+    }
+    bar();
+    char* img = smem + wid * 16384;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ng = n0 + wn * 64 + j * 16 + fq * 4;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = i * 16 + fr;
+            const int c8 = (j * 4 + fq) ^ (row & 15);
+            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
+                make_uint2(pack_bf2(acc[j][i][0] + bv.x, acc[j][i][1] + bv.y), pack_bf2(acc[j][i][2] + bv.z, acc[j][i][3] + bv.w));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int c16 = lane & 7;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+        const int row = it * 8 + (lane >> 3);
+        uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+        if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+        const int m = m0 + wm * 128 + row, n = n0 + wn * 64 + c16 * 8;
+        if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * N + n) = v;
+    }
+}
+
+
+// ---------------------------------------------------------------- V11: ping-pong with quadrant phases
+// Per K-tile 4 phases per wave, each computing one 64 x 32 C-quadrant over K = 64 (16 MFMAs). Quadrant order
+// (0,0) (0,1) (1,1) (1,0): fragment reads per load segment 12 / 4 / 8 / 4. DMA pieces of tile k+1 issued
+// 3 / 3 / 2 / 0 over the load segments of tile k; group 0 retires after compute phase 3, group 1 after load
+// phase 3 (one segment before group 0's first read of tile k+1).
+__global__ __launch_bounds__(512) void k_v11(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                             const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[LDSB];
+    const int wid0 = threadIdx.x >> 6;
+    const int grp = wid0 >> 2;
+    Ctx c = make_ctx(A, W, M, N, K, grp, wid0 & 3);
+    const bool g1 = __builtin_amdgcn_readfirstlane(grp) == 1;
+    uint32_t oa[4], ob[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        oa[i] = dma_off(i * 8 + c.wid, c.lane, M - 1 - c.m0, K);
+        ob[i] = dma_off(i * 8 + c.wid, c.lane, N - 1 - c.n0, K);
+    }
+    auto piece = [&](int buf, int kt, int p) {
+        char* na = smem + buf * STB;
+        const uint32_t koff = (uint32_t)kt * (BK * 2);
+        if (p < 4) dma(c.Ablk, oa[p] + koff, na + (p * 8 + c.wid) * 1024);
+        else dma(c.Bblk, ob[p - 4] + koff, na + OPB + ((p - 4) * 8 + c.wid) * 1024);
+    };
+    const int sw = (c.fr >> 1) & 7;
+    const int abase = (c.wm * 128 + c.fr) * 128, bbase = OPB + (c.wn * 64 + c.fr) * 128;
+    const int ch0 = (c.fq ^ sw) << 4, ch1 = ((4 + c.fq) ^ sw) << 4;
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = K / BK;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) piece(0, 0, p);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (g1) bar();
+    bf16x8 am[4][2], bn0[2][2], bn1[2][2];   // A rows of one mq half (4 frags x 2 ks), B cols of nq halves
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* base = smem + (kt & 1) * STB;
+        const bool pre = kt + 1 < nk;
+        const int nb = (kt + 1) & 1;
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+            const int mq = (ph == 0 || ph == 1) ? 0 : 1;
+            const int nq = (ph == 0 || ph == 3) ? 0 : 1;
+            // ---- load segment
+            if (ph == 0 || ph == 2) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    am[i][0] = *reinterpret_cast<const bf16x8*>(base + abase + (mq * 4 + i) * 2048 + ch0);
+                    am[i][1] = *reinterpret_cast<const bf16x8*>(base + abase + (mq * 4 + i) * 2048 + ch1);
+                }
+            }
+            if (ph != 2) {
+                bf16x8 (&bn)[2][2] = nq ? bn1 : bn0;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    bn[j][0] = *reinterpret_cast<const bf16x8*>(base + bbase + (nq * 2 + j) * 2048 + ch0);
+                    bn[j][1] = *reinterpret_cast<const bf16x8*>(base + bbase + (nq * 2 + j) * 2048 + ch1);
+                }
+            }
+            if (pre) {
+                if (ph == 0) { piece(nb, kt + 1, 0); piece(nb, kt + 1, 1); piece(nb, kt + 1, 2); }
+                if (ph == 1) { piece(nb, kt + 1, 3); piece(nb, kt + 1, 4); piece(nb, kt + 1, 5); }
+                if (ph == 2) { piece(nb, kt + 1, 6); piece(nb, kt + 1, 7); }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (g1 && ph == 3 && pre) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();
+            // ---- compute segment: quadrant (mq, nq) over K = 64
+            __builtin_amdgcn_s_setprio(1);
+            const bf16x8 (&bq)[2][2] = nq ? bn1 : bn0;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        acc[nq * 2 + j][mq * 4 + i] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j][ks], am[i][ks], acc[nq * 2 + j][mq * 4 + i], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            if (!g1 && ph == 3 && pre) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();
+        }
+    }
+    if (!g1) bar();
+    epilogue(smem, acc, c, bias, C, M, N);
+}
+
+// ---------------------------------------------------------------- V0 with s_memtime stamps (diagnostic)
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+__global__ __launch_bounds__(512) void k_v0_stamped(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                    const float* __restrict__ bias, bf16_t* C, int M, int N, int K,
+                                                    unsigned long long* dbg) {
+    __shared__ __attribute__((aligned(16))) char smem[LDSB];
+    const unsigned long long tk0 = stamp();
+    const int wid0 = threadIdx.x >> 6;
+    Ctx c = make_ctx(A, W, M, N, K, wid0 >> 2, wid0 & 3);
+    uint32_t oa[4], ob[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        oa[i] = dma_off(i * 8 + c.wid, c.lane, M - 1 - c.m0, K);
+        ob[i] = dma_off(i * 8 + c.wid, c.lane, N - 1 - c.n0, K);
+    }
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = K / BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        dma(c.Ablk, oa[i], smem + (i * 8 + c.wid) * 1024);
+        dma(c.Bblk, ob[i], smem + OPB + (i * 8 + c.wid) * 1024);
+    }
+    unsigned long long s_wait = 0, s_issue = 0, s_comp = 0, s_first = 0;
+    const unsigned long long tloop = stamp();
+    for (int kt = 0; kt < nk; ++kt) {
+        const unsigned long long t0 = stamp();
+        __syncthreads();
+        const unsigned long long t1 = stamp();
+        const char* la = smem + (kt & 1) * STB;
+        const char* lb = la + OPB;
+        char* na = smem + ((kt + 1) & 1) * STB;
+        const uint32_t koff = (uint32_t)(kt + 1) * (BK * 2);
+        if (kt + 1 < nk) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                dma(c.Ablk, oa[i] + koff, na + (i * 8 + c.wid) * 1024);
+                dma(c.Bblk, ob[i] + koff, na + OPB + (i * 8 + c.wid) * 1024);
+            }
+        }
+        const unsigned long long t2 = stamp();
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 a[8], b[4];
+            read_frags(la, lb, ks, c, a, b);
+            mfma32(acc, a, b);
+        }
+        // make the stamp wait for the MFMAs: consume one accumulator
+        asm volatile("" :: "v"(acc[3][7]));
+        const unsigned long long t3 = stamp();
+        s_wait += t1 - t0; s_issue += t2 - t1; s_comp += t3 - t2;
+        if (kt == 0) s_first = t1 - tloop;
+    }
+    const unsigned long long tep = stamp();
+    epilogue(smem, acc, c, bias, C, M, N);
+    const unsigned long long tend = stamp();
+    if (c.lane == 0) {
+        unsigned long long* d = dbg + ((size_t)blockIdx.x * 8 + c.wid) * 8;
+        d[0] = tloop - tk0; d[1] = s_wait; d[2] = s_issue; d[3] = s_comp; d[4] = tend - tep; d[5] = tend - tk0;
+        d[6] = s_first; d[7] = tk0;
+    }
+}
+
+__global__ __launch_bounds__(512) void k_v10s(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                             const float* __restrict__ bias, bf16_t* C, int M, int N, int K,
+                                             unsigned long long* dbg) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * V9_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool loader = wid >= 4;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tiles_n = (N + 127) / 128;
+    const int tm = lid / tiles_n, tn = lid - tm * tiles_n;
+    const int m0 = tm * 256, n0 = tn * 128;
+    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * K * 2;
+    const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2;
+    const int nk = K / 64;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int wm = (wid & 3) >> 1, wn = wid & 1;
+
+    if (loader) {
+        const int lw = wid - 4;
+        uint32_t oa[8], ob[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) oa[i] = dma_off(i * 4 + lw, lane, M - 1 - m0, K);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ob[i] = dma_off(i * 4 + lw, lane, N - 1 - n0, K);
+        auto issue = [&](int st) {
+            char* d = smem + (st % 3) * V9_STAGE;
+            const uint32_t koff = (uint32_t)st * 128;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dma(Ablk, oa[i] + koff, d + (i * 4 + lw) * 1024);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dma(Bblk, ob[i] + koff, d + 32768 + (i * 4 + lw) * 1024);
+        };
+        issue(0);
+        if (nk > 1) issue(1);
+        if (nk > 1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();                                      // X_-1: stage 0 landed
+        unsigned long long t_issue = 0, t_vm = 0, t_bar = 0;
+        for (int st = 0; st + 1 < nk; ++st) {
+            const unsigned long long t0 = stamp();
+            if (st + 2 < nk) issue(st + 2);
+            const unsigned long long t1 = stamp();
+            if (st + 2 < nk) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned long long t2 = stamp();
+            bar();
+            const unsigned long long t3 = stamp();
+            t_issue += t1 - t0; t_vm += t2 - t1; t_bar += t3 - t2;
+        }
+        if (lane == 0) { unsigned long long* d = dbg + ((size_t)blockIdx.x * 8 + wid) * 4; d[0] = t_issue; d[1] = t_vm; d[2] = t_bar; d[3] = 1; }
+        bar();                                      // epilogue
+        return;
+    }
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int sw = (fr >> 1) & 7;
+    const int aoff0 = (wm * 128 + fr) * 128 + ((fq ^ sw) << 4), aoff1 = (wm * 128 + fr) * 128 + (((4 + fq) ^ sw) << 4);
+    const int boff0 = 32768 + (wn * 64 + fr) * 128 + ((fq ^ sw) << 4), boff1 = 32768 + (wn * 64 + fr) * 128 + (((4 + fq) ^ sw) << 4);
+    auto rd = [&](const char* la, int half, bf16x8 a[8], bf16x8 b[4]) {
+        const char* pa = la + (half ? aoff1 : aoff0);
+        const char* pb = la + (half ? boff1 : boff0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(pa + i * 2048);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(pb + j * 2048);
+    };
+    bar();                                          // X_-1
+    bf16x8 a0[8], b0[4], a1[8], b1[4];
+    rd(smem, 0, a0, b0);
+    unsigned long long t_m1 = 0, t_bar = 0, t_m2 = 0;
+    for (int st = 0; st < nk; ++st) {
+        const char* la = smem + (st % 3) * V9_STAGE;
+        const unsigned long long t0 = stamp();
+        rd(la, 1, a1, b1);
+        mfma32(acc, a0, b0);
+        asm volatile("" :: "v"(acc[3][7]));
+        const unsigned long long t1 = stamp();
+        if (st + 1 < nk) {
+            bar();
+            rd(smem + ((st + 1) % 3) * V9_STAGE, 0, a0, b0);
+        }
+        const unsigned long long t2 = stamp();
+        mfma32(acc, a1, b1);
+        asm volatile("" :: "v"(acc[3][7]));
+        const unsigned long long t3 = stamp();
+        t_m1 += t1 - t0; t_bar += t2 - t1; t_m2 += t3 - t2;
+    }
+    if (lane == 0) { unsigned long long* d = dbg + ((size_t)blockIdx.x * 8 + wid) * 4; d[0] = t_m1; d[1] = t_bar; d[2] = t_m2; d[3] = 0; }
+    bar();
+    char* img = smem + wid * 16384;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ng = n0 + wn * 64 + j * 16 + fq * 4;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = i * 16 + fr;
+            const int c8 = (j * 4 + fq) ^ (row & 15);
+            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
+                make_uint2(pack_bf2(acc[j][i][0] + bv.x, acc[j][i][1] + bv.y), pack_bf2(acc[j][i][2] + bv.z, acc[j][i][3] + bv.w));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int c16 = lane & 7;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+        const int row = it * 8 + (lane >> 3);
+        uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+        if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+        const int m = m0 + wm * 128 + row, n = n0 + wn * 64 + c16 * 8;
+        if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * N + n) = v;
+    }
+}
+
+
 // ---------------------------------------------------------------- host
 static void fill_bf16(std::vector<bf16_t>& v, float scale, unsigned seed) {
     std::mt19937 g(seed);
@@ -393,11 +1086,12 @@ int main(int argc, char** argv) {
     struct Shape { const char* name; int M, N, K; };
     const int Mtok = 4096 * 197;
     Shape shapes[] = {{"qkv", Mtok, 2304, 768}, {"proj", Mtok, 768, 768}, {"fc1", Mtok, 3072, 768},
-                      {"fc2", Mtok, 768, 3072}};
+                      {"fc2", Mtok, 768, 3072}, {"small_qkv", 16384, 2304, 768}, {"small_fc2", 65536, 768, 3072}};
     struct Var { const char* name; kfn f; };
     Var vars[] = {{"V0", k_v01<false>}, {"V1", k_v01<true>}, {"V2", k_pp<false>}, {"V3", k_pp<true>},
                   {"V4r4", k_ring<4, false>}, {"V4r5", k_ring<5, false>}, {"V5r4", k_ring<4, true>},
-                  {"V5r5", k_ring<5, true>}};
+                  {"V5r5", k_ring<5, true>}, {"V7", k_v7<false>}, {"V7p", k_v7<true>},
+                  {"V0samek", k_v01<false, true>}, {"V8", k_v8}, {"V9", k_v9}, {"V10", k_v10}, {"V11", k_v11}};
     const int NV = sizeof(vars) / sizeof(vars[0]);
     size_t maxA = 0, maxW = 0, maxC = 0;
     for (auto& s : shapes) {
@@ -406,6 +1100,7 @@ int main(int argc, char** argv) {
     }
     std::vector<bf16_t> hA(maxA), hW(maxW);
     fill_bf16(hA, 1.0f, 1); fill_bf16(hW, 0.05f, 2);
+    if (getenv("LAB_ZERO")) { std::fill(hA.begin(), hA.end(), 0); std::fill(hW.begin(), hW.end(), 0); }
     std::vector<float> hb(4096, 0.01f);
     bf16_t *dA, *dW, *dC0, *dC;
     float* db;
@@ -420,6 +1115,8 @@ int main(int argc, char** argv) {
     for (auto& s : shapes) {
         if (shape_filter[0] && !strstr(shape_filter, s.name)) continue;
         const int tiles = ((s.M + BM - 1) / BM) * ((s.N + BN - 1) / BN);
+        const int tiles128 = ((s.M + BM - 1) / BM) * ((s.N + 127) / 128);
+        auto grid_of = [&](int v) { return dim3((strcmp(vars[v].name, "V9") == 0 || strcmp(vars[v].name, "V10") == 0) ? tiles128 : tiles); };
         const double flop = 2.0 * s.M * (double)s.N * s.K;
         std::vector<std::vector<float>> ms(NV);
         auto on = [&](int v) { return !var_filter[0] || strstr(var_filter, vars[v].name); };
@@ -430,7 +1127,7 @@ int main(int argc, char** argv) {
         CHECK(hipMemcpy(ref.data(), dC0, (size_t)s.M * s.N * 2, hipMemcpyDeviceToHost));
         for (int v = 1; v < NV; ++v) {
             CHECK(hipMemset(dC, 0, (size_t)s.M * s.N * 2));
-            hipLaunchKernelGGL(vars[v].f, dim3(tiles), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
+            hipLaunchKernelGGL(vars[v].f, grid_of(v), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
             CHECK(hipDeviceSynchronize());
             CHECK(hipMemcpy(got.data(), dC, (size_t)s.M * s.N * 2, hipMemcpyDeviceToHost));
             size_t bad = 0;
@@ -443,7 +1140,7 @@ int main(int argc, char** argv) {
                 if (!on(v)) { ms[v].push_back(0.f); continue; }
                 CHECK(hipEventRecord(e0, 0));
                 for (int it = 0; it < 3; ++it)
-                    hipLaunchKernelGGL(vars[v].f, dim3(tiles), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
+                    hipLaunchKernelGGL(vars[v].f, grid_of(v), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
                 CHECK(hipEventRecord(e1, 0));
                 CHECK(hipEventSynchronize(e1));
                 float t; CHECK(hipEventElapsedTime(&t, e0, e1));
@@ -456,6 +1153,48 @@ int main(int argc, char** argv) {
                    s.K, med, flop / (med * 1e-3) / 1e12, ms[v][0]);
         }
         fflush(stdout);
+    }
+    if (getenv("LAB_STAMPS10")) {
+        for (auto& s : shapes) {
+            if (shape_filter[0] && !strstr(shape_filter, s.name)) continue;
+            const int tiles = ((s.M + BM - 1) / BM) * ((s.N + 127) / 128);
+            unsigned long long* dbg;
+            CHECK(hipMalloc(&dbg, (size_t)tiles * 32 * 8));
+            for (int rep = 0; rep < 2; ++rep)
+                hipLaunchKernelGGL(k_v10s, dim3(tiles), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K, dbg);
+            CHECK(hipDeviceSynchronize());
+            std::vector<unsigned long long> h((size_t)tiles * 32);
+            CHECK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+            double c[3] = {0}, l[3] = {0};
+            for (int t = 0; t < tiles; ++t)
+                for (int w = 0; w < 8; ++w)
+                    for (int k = 0; k < 3; ++k) (w < 4 ? c : l)[k] += (double)h[((size_t)t * 8 + w) * 4 + k];
+            const double nb = (double)tiles * 4 * (s.K / 64);
+            printf("V10 stamps %s per stage (cycles): consumer mfma1(+rd) %.0f bar(+rd0) %.0f mfma2 %.0f | loader issue %.0f vmwait %.0f bar %.0f\n",
+                   s.name, c[0] / nb, c[1] / nb, c[2] / nb, l[0] / nb, l[1] / nb, l[2] / nb);
+            CHECK(hipFree(dbg));
+        }
+    }
+    if (getenv("LAB_STAMPS")) {
+        for (auto& s : shapes) {
+            if (shape_filter[0] && !strstr(shape_filter, s.name)) continue;
+            const int tiles = ((s.M + BM - 1) / BM) * ((s.N + BN - 1) / BN);
+            unsigned long long* dbg;
+            CHECK(hipMalloc(&dbg, (size_t)tiles * 64 * 8));
+            for (int rep = 0; rep < 2; ++rep)
+                hipLaunchKernelGGL(k_v0_stamped, dim3(tiles), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K, dbg);
+            CHECK(hipDeviceSynchronize());
+            std::vector<unsigned long long> h((size_t)tiles * 64);
+            CHECK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+            double acc[8] = {0};
+            for (int t = 0; t < tiles; ++t)
+                for (int w = 0; w < 8; ++w)
+                    for (int k = 0; k < 7; ++k) acc[k] += (double)h[((size_t)t * 8 + w) * 8 + k];
+            const double nb = (double)tiles * 8;
+            printf("stamps %s (per wave, avg cycles): prologue %.0f | loop: wait %.0f issue %.0f compute %.0f (first wait %.0f) | epilogue %.0f | total %.0f\n",
+                   s.name, acc[0] / nb, acc[1] / nb, acc[2] / nb, acc[3] / nb, acc[6] / nb, acc[4] / nb, acc[5] / nb);
+            CHECK(hipFree(dbg));
+        }
     }
     return 0;
 }

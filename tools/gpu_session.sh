@@ -22,6 +22,9 @@ for step in "$@"; do
     bench)
       timeout -k 10 900 python bench.py --steps 5 --warmup 2 > $OUT/bench.log 2>&1
       ok_or_stop $? bench; tail -3 $OUT/bench.log ;;
+    bench_np)
+      VPF_GEMM_PERSISTENT=0 timeout -k 10 900 python bench.py --steps 5 --warmup 2 --cpu-seconds 0 > $OUT/bench_np.log 2>&1
+      ok_or_stop $? bench_np; tail -1 $OUT/bench_np.log | cut -c1-400 ;;
     prof)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/prof.log 2>&1

@@ -18,6 +18,7 @@
 //    fully coalesced 16-B row stores (+ 16-B residual reads / position-embedding adds).
 //  * Workgroup -> tile mapping is XCD-aware (bijective remap, cdna_hip_programming.md §5 T1): the blocks
 //    that share an XCD walk consecutive tiles of one 256-row A panel, so the panel is an L2 hit.
+#include <stdlib.h>
 #include "vpf_common.h"
 #include "../../include/vpf.h"
 
@@ -243,11 +244,248 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------
+// Persistent variant: one workgroup per CU walks its XCD's tiles; the (tile, K-step) sequence is one flat
+// pipeline, so the DMA of the next tile's first K-tile flies during the current tile's epilogue and no
+// workgroup launch / drain separates tiles. Epilogue staged through the free stage of the ring in two
+// halves (8 KiB image per wave), each wave reading back only its own image (no block barrier needed).
+// Tile assignment: tiles are cut into 8 contiguous chunks, one per XCD group (blocks b, b+8, ... share an
+// XCD); the k-th block of a group takes tiles chunk_start + k + r * blocks_in_group, so the blocks running
+// together on an XCD work on consecutive tiles (shared A panel / W panels in that XCD's L2).
+template <int EPI>
+__global__ __launch_bounds__(NTHREADS) void k_gemm_bf16_pers(const bf16_t* __restrict__ A, int lda,
+                                                             const bf16_t* __restrict__ W,
+                                                             const float* __restrict__ bias,
+                                                             const bf16_t* residual,
+                                                             const float* __restrict__ pos, int g2,
+                                                             const float2* __restrict__ stats,
+                                                             const float* __restrict__ colsum,
+                                                             bf16_t* C, int ldc, int M, int N, int K, int tiles) {
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 2, wn = wid & 3;
+    const int fr = lane & 15, fq = lane >> 4;
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+
+    const int G = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, kx = bid >> 3;
+    const int nbx = (G >> 3) + (xcd < (G & 7) ? 1 : 0);
+    const int tq = tiles >> 3, tr = tiles & 7;
+    const int t_start = xcd < tr ? xcd * (tq + 1) : tr * (tq + 1) + (xcd - tr) * tq;
+    const int t_count = tq + (xcd < tr ? 1 : 0);
+    const int my_tiles = kx < t_count ? (t_count - kx + nbx - 1) / nbx : 0;
+    const int nk = K / BK;
+    const int total = my_tiles * nk;
+    if (total == 0) return;
+    const int tiles_n = (N + BN - 1) / BN;
+
+    // per-lane DMA geometry (tile independent): rows 8g + (lane >> 3) of wave-instructions g = i*8 + wid
+    int drow[4], dlch[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        drow[i] = 8 * (i * 8 + wid) + (lane >> 3);
+        dlch[i] = ((lane & 7) ^ ((drow[i] >> 1) & 7)) * 16;
+    }
+    auto tile_of = [&](int r, int& m0, int& n0) {
+        const int t = t_start + kx + r * nbx;
+        const int tm = t / tiles_n;
+        m0 = tm * BM; n0 = (t - tm * tiles_n) * BN;
+    };
+    auto issue = [&](int st) {
+        const int r = st / nk, kt = st - r * nk;
+        int m0, n0;
+        tile_of(r, m0, n0);
+        const char* Ab = reinterpret_cast<const char*>(A) + (size_t)m0 * lda * 2 + (size_t)kt * (BK * 2);
+        const char* Bb = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2 + (size_t)kt * (BK * 2);
+        char* la = smem + (st & 1) * STAGE_BYTES;
+        char* lb = la + OPERAND_BYTES;
+        const int ra_max = M - 1 - m0, rb_max = N - 1 - n0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int g = i * 8 + wid;
+            const uint32_t oa = (uint32_t)min(drow[i], ra_max) * (uint32_t)(lda * 2) + (uint32_t)dlch[i];
+            const uint32_t ob = (uint32_t)min(drow[i], rb_max) * (uint32_t)(K * 2) + (uint32_t)dlch[i];
+            __builtin_amdgcn_global_load_lds((gptr_t)(Ab + oa), (lptr_t)(la + g * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)(Bb + ob), (lptr_t)(lb + g * 1024), 16, 0, 0);
+        }
+    };
+    float4 bv[4], cv[4];
+    float2 rs[8];
+    auto load_epi = [&](int m0, int n0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ng = n0 + wn * 64 + j * 16 + fq * 4;
+            bv[j] = ng < N ? *reinterpret_cast<const float4*>(bias + ng) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (LN) cv[j] = ng < N ? *reinterpret_cast<const float4*>(colsum + ng) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if constexpr (LN) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int m = m0 + wm * 128 + i * 16 + fr;
+                const float2 st = m < M ? stats[m] : make_float2(0.f, 0.f);
+                rs[i] = make_float2(st.y, -st.y * st.x);
+            }
+        }
+    };
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int cm0, cn0;
+    tile_of(0, cm0, cn0);
+    issue(0);
+    load_epi(cm0, cn0);
+    int kt = 0, r = 0;
+    for (int st = 0; st < total; ++st) {
+        __syncthreads();   // K-step st landed for every wave; stage (st+1)&1 fully read
+        if (st + 1 < total) issue(st + 1);
+        const char* la = smem + (st & 1) * STAGE_BYTES;
+        const char* lb = la + OPERAND_BYTES;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 a[8], b[4];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = wm * 128 + i * 16 + fr;
+                a[i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + (((ks * 4 + fq) ^ ((row >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = wn * 64 + j * 16 + fr;
+                b[j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + (((ks * 4 + fq) ^ ((row >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
+        }
+        if (++kt < nk) continue;
+        // ---------------- tile epilogue (stage st&1 is free once every wave is past this barrier) ----------
+        kt = 0;
+        __syncthreads();
+        char* img = smem + (st & 1) * STAGE_BYTES + wid * 8192;
+        const int c16 = lane & 7;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii) {
+                    const int i = hf * 4 + ii;
+                    float v0, v1, v2, v3;
+                    if constexpr (LN) {
+                        v0 = fmaf(rs[i].x, acc[j][i][0], fmaf(rs[i].y, cv[j].x, bv[j].x));
+                        v1 = fmaf(rs[i].x, acc[j][i][1], fmaf(rs[i].y, cv[j].y, bv[j].y));
+                        v2 = fmaf(rs[i].x, acc[j][i][2], fmaf(rs[i].y, cv[j].z, bv[j].z));
+                        v3 = fmaf(rs[i].x, acc[j][i][3], fmaf(rs[i].y, cv[j].w, bv[j].w));
+                    } else {
+                        v0 = acc[j][i][0] + bv[j].x; v1 = acc[j][i][1] + bv[j].y;
+                        v2 = acc[j][i][2] + bv[j].z; v3 = acc[j][i][3] + bv[j].w;
+                    }
+                    if constexpr (EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU) {
+                        const f32x2 g01 = gelu_erf2(f32x2{v0, v1}), g23 = gelu_erf2(f32x2{v2, v3});
+                        v0 = g01.x; v1 = g01.y; v2 = g23.x; v3 = g23.y;
+                    }
+                    const int row = ii * 16 + fr;
+                    const int c8 = (j * 4 + fq) ^ (row & 15);
+                    *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+                }
+            }
+            uint4 res[8];
+            if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int m = cm0 + wm * 128 + hf * 64 + it * 8 + (lane >> 3);
+                    const int n = cn0 + wn * 64 + c16 * 8;
+                    res[it] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(residual + (int64_t)m * ldc + n)
+                                               : make_uint4(0, 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int it = 0; it < 8; ++it) {
+                const int row = it * 8 + (lane >> 3);
+                uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+                if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+                const int m = cm0 + wm * 128 + hf * 64 + row;
+                const int n = cn0 + wn * 64 + c16 * 8;
+                if (m >= M || n >= N) continue;
+                int64_t orow = m;
+                if constexpr (EPI == VPF_EPI_PATCH) {
+                    const int pi = m % g2;
+                    orow = (int64_t)(m / g2) * (g2 + 1) + 1 + pi;
+                    const float* pr = pos + (int64_t)(1 + pi) * N + n;
+                    const float4 p0 = *reinterpret_cast<const float4*>(pr);
+                    const float4 p1 = *reinterpret_cast<const float4*>(pr + 4);
+                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                    const float pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+                    uint32_t o[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        o[e] = pack_bf2(bf2f((bf16_t)(w[e] & 0xffff)) + pv[2 * e], bf2f((bf16_t)(w[e] >> 16)) + pv[2 * e + 1]);
+                    v = make_uint4(o[0], o[1], o[2], o[3]);
+                }
+                if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
+                    const uint4 rv = res[it];
+                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                    const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+                    uint32_t o[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        o[e] = pack_bf2(bf2f((bf16_t)(w[e] & 0xffff)) + bf2f((bf16_t)(rr[e] & 0xffff)),
+                                        bf2f((bf16_t)(w[e] >> 16)) + bf2f((bf16_t)(rr[e] >> 16)));
+                    v = make_uint4(o[0], o[1], o[2], o[3]);
+                }
+                *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (++r < my_tiles) {
+            tile_of(r, cm0, cn0);
+            load_epi(cm0, cn0);
+        }
+    }
+}
+
 }  // namespace
 
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
-    hipLaunchKernelGGL(k_gemm_bf16<E>, grid, block, 0, s, A, (int)lda, W, bias, residual, pos, patch_rows,         \
-                       reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k)
+    do {                                                                                                     \
+        if (pers)                                                                                            \
+            hipLaunchKernelGGL(k_gemm_bf16_pers<E>, pgrid, block, 0, s, A, (int)lda, W, bias, residual, pos,   \
+                               patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, \
+                               k, (int)tiles);                                                               \
+        else                                                                                                 \
+            hipLaunchKernelGGL(k_gemm_bf16<E>, grid, block, 0, s, A, (int)lda, W, bias, residual, pos, patch_rows, \
+                               reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k);    \
+    } while (0)
+
+// VPF_GEMM_PERSISTENT=1 selects the persistent kernel (one workgroup per CU); the default is one tile per
+// workgroup, which measured faster on the ViT-B encoder shapes (5.69 vs 5.43 frames/s, profiles/r1_notes.md).
+static int cu_count() {
+    static int cached = 0;
+    if (!cached) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        cached = n;
+    }
+    return cached;
+}
+static bool use_persistent() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("VPF_GEMM_PERSISTENT"); v = (e && e[0] == '1') ? 1 : 0; }
+    return v == 1;
+}
 
 VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, const float* bias,
                           const uint16_t* residual, const float* pos, int patch_rows, const float* row_stats,
@@ -266,6 +504,8 @@ VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, con
     if (tiles > INT32_MAX) return VPF_ERR_ARG;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)tiles), block(NTHREADS);
+    const bool pers = use_persistent();
+    const dim3 pgrid((unsigned)(tiles < cu_count() ? tiles : cu_count()));
     const int m = (int)M, n = (int)N, k = (int)K;
     switch (epilogue) {
         case VPF_EPI_BIAS: VPF_GEMM_LAUNCH(VPF_EPI_BIAS); break;
