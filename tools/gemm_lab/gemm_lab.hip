@@ -101,6 +101,43 @@ __device__ __forceinline__ void mfma32(f32x4 acc[4][8], const bf16x8 a[8], const
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// G = 1: product GELU (A&S 7.1.26, packed; 2 transcendentals per element)
+__device__ __forceinline__ f32x2 gelu_as26(f32x2 x) {
+    const f32x2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+    const f32x2 den = z * 0.3275911f + 1.0f;
+    const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    f32x2 p = t * 1.061405429f - 1.453152027f;
+    p = p * t + 1.421413741f;
+    p = p * t - 0.284496736f;
+    p = p * t + 0.254829592f;
+    p = p * t;
+    const f32x2 ez = z * z * -1.44269504088896341f;
+    const f32x2 e = {__builtin_amdgcn_exp2f(ez.x), __builtin_amdgcn_exp2f(ez.y)};
+    const f32x2 erf_abs = 1.0f - p * e;
+    const f32x2 half = {__builtin_copysignf(0.5f, x.x), __builtin_copysignf(0.5f, x.y)};
+    return x * (half * erf_abs + 0.5f);
+}
+// G = 2: A&S 7.1.28, erfc(z) = (1 + a1 z + ... + a6 z^6)^-16 (|err| <= 3e-7), one rcp per element. The factor
+// 2^(1/16) folded into the coefficients makes the reciprocal 0.5 erfc directly: Phi(x) = x<0 ? h : 1-h.
+__device__ __forceinline__ f32x2 gelu_as28(f32x2 x) {
+    constexpr float c = 1.0442737824274138f;   // 2^(1/16)
+    constexpr float s = 0.70710678118654752f;
+    const f32x2 z = __builtin_elementwise_abs(x);
+    f32x2 p = z * (0.0000430638f * c * s * s * s * s * s * s) + (0.0002765672f * c * s * s * s * s * s);
+    p = p * z + (0.0001520143f * c * s * s * s * s);
+    p = p * z + (0.0092705272f * c * s * s * s);
+    p = p * z + (0.0422820123f * c * s * s);
+    p = p * z + (0.0705230784f * c * s);
+    p = p * z + c;
+    p = p * p; p = p * p; p = p * p; p = p * p;
+    const f32x2 h = {__builtin_amdgcn_rcpf(p.x), __builtin_amdgcn_rcpf(p.y)};
+    const f32x2 q = 0.5f - h;
+    const f32x2 sq = {__builtin_copysignf(q.x, x.x), __builtin_copysignf(q.y, x.y)};
+    return x * (sq + 0.5f);
+}
+
+template <int G = 0>
 __device__ __forceinline__ void epilogue(char* smem, f32x4 acc[4][8], const Ctx& c, const float* bias, bf16_t* C,
                                          int M, int N) {
     __syncthreads();
@@ -114,8 +151,11 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 acc[4][8], const Ctx&
         for (int i = 0; i < 8; ++i) {
             const int row = i * 16 + c.fr;
             const int c8 = (j * 4 + c.fq) ^ (row & 15);
+            f32x2 v01 = {acc[j][i][0] + bv.x, acc[j][i][1] + bv.y}, v23 = {acc[j][i][2] + bv.z, acc[j][i][3] + bv.w};
+            if constexpr (G == 1) { v01 = gelu_as26(v01); v23 = gelu_as26(v23); }
+            if constexpr (G == 2) { v01 = gelu_as28(v01); v23 = gelu_as28(v23); }
             *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
-                make_uint2(pack_bf2(acc[j][i][0] + bv.x, acc[j][i][1] + bv.y), pack_bf2(acc[j][i][2] + bv.z, acc[j][i][3] + bv.w));
+                make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
         }
     }
     __syncthreads();
@@ -131,7 +171,7 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 acc[4][8], const Ctx&
 }
 
 // ---------------------------------------------------------------- V0 / V1
-template <bool SPREAD, bool SAMEK = false>
+template <bool SPREAD, bool SAMEK = false, int G = 0>
 __global__ __launch_bounds__(512) void k_v01(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                              const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
     __shared__ __attribute__((aligned(16))) char smem[LDSB];
@@ -187,7 +227,7 @@ __global__ __launch_bounds__(512) void k_v01(const bf16_t* __restrict__ A, const
             if (SPREAD) __builtin_amdgcn_s_setprio(0);
         }
     }
-    epilogue(smem, acc, c, bias, C, M, N);
+    epilogue<G>(smem, acc, c, bias, C, M, N);
 }
 
 // ---------------------------------------------------------------- V2 / V3 ping-pong
@@ -765,8 +805,11 @@ __global__ __launch_bounds__(512) void k_v10(const bf16_t* __restrict__ A, const
         for (int i = 0; i < 8; ++i) {
             const int row = i * 16 + fr;
             const int c8 = (j * 4 + fq) ^ (row & 15);
+            f32x2 v01 = {acc[j][i][0] + bv.x, acc[j][i][1] + bv.y}, v23 = {acc[j][i][2] + bv.z, acc[j][i][3] + bv.w};
+            if constexpr (false) { v01 = gelu_as26(v01); v23 = gelu_as26(v23); }
+            if constexpr (false) { v01 = gelu_as28(v01); v23 = gelu_as28(v23); }
             *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
-                make_uint2(pack_bf2(acc[j][i][0] + bv.x, acc[j][i][1] + bv.y), pack_bf2(acc[j][i][2] + bv.z, acc[j][i][3] + bv.w));
+                make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1048,8 +1091,11 @@ __global__ __launch_bounds__(512) void k_v10s(const bf16_t* __restrict__ A, cons
         for (int i = 0; i < 8; ++i) {
             const int row = i * 16 + fr;
             const int c8 = (j * 4 + fq) ^ (row & 15);
+            f32x2 v01 = {acc[j][i][0] + bv.x, acc[j][i][1] + bv.y}, v23 = {acc[j][i][2] + bv.z, acc[j][i][3] + bv.w};
+            if constexpr (false) { v01 = gelu_as26(v01); v23 = gelu_as26(v23); }
+            if constexpr (false) { v01 = gelu_as28(v01); v23 = gelu_as28(v23); }
             *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
-                make_uint2(pack_bf2(acc[j][i][0] + bv.x, acc[j][i][1] + bv.y), pack_bf2(acc[j][i][2] + bv.z, acc[j][i][3] + bv.w));
+                make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1066,6 +1112,75 @@ __global__ __launch_bounds__(512) void k_v10s(const bf16_t* __restrict__ A, cons
 
 
 // ---------------------------------------------------------------- host
+
+// ---------------------------------------------------------------- V12: occupancy 2
+// 256x128x32 tile, 4 waves (each the same 128x64 sub-tile as V0), 2-stage ring of 64-B rows (16-B chunk c of
+// row r at c ^ F[(r >> 2) & 3], conflict-free per tools/lds_banks.py), 64 KiB LDS -> two workgroups per CU,
+// so one workgroup's barrier waits and epilogue overlap the other's MFMA stream.
+constexpr int V12_A = 256 * 64, V12_STAGE = 384 * 64;   // bytes
+__device__ __forceinline__ int f64sw(int r) { return (0x1E0 >> (2 * ((r >> 2) & 3))) & 3; }   // F = {0,2,3,1}
+__device__ __forceinline__ uint32_t dma_off_r64(int g, int lane, int rows_left, int K) {
+    const int row = 16 * g + (lane >> 2);
+    const int ch = (lane & 3) ^ f64sw(row);
+    return (uint32_t)min(row, rows_left) * (uint32_t)(K * 2) + (uint32_t)(ch * 16);
+}
+template <int G = 0>
+__global__ __launch_bounds__(256, 2) void k_v12(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                const float* __restrict__ bias, bf16_t* C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[65536];
+    Ctx c;
+    {
+        const int nwg = gridDim.x, bid = blockIdx.x;
+        const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+        const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+        const int tiles_n = (N + 127) / 128;
+        const int tm = lid / tiles_n, tn = lid - tm * tiles_n;
+        c.m0 = tm * 256; c.n0 = tn * 128;
+        c.lane = threadIdx.x & 63;
+        c.wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        c.wm = c.wid >> 1; c.wn = c.wid & 1; c.fr = c.lane & 15; c.fq = c.lane >> 4;
+        c.Ablk = reinterpret_cast<const char*>(A) + (size_t)c.m0 * K * 2;
+        c.Bblk = reinterpret_cast<const char*>(W) + (size_t)c.n0 * K * 2;
+    }
+    uint32_t oa[4], ob[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) oa[i] = dma_off_r64(i * 4 + c.wid, c.lane, M - 1 - c.m0, K);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ob[i] = dma_off_r64(i * 4 + c.wid, c.lane, N - 1 - c.n0, K);
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = K / 32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma(c.Ablk, oa[i], smem + (i * 4 + c.wid) * 1024);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma(c.Bblk, ob[i], smem + V12_A + (i * 4 + c.wid) * 1024);
+    const int sw = f64sw(c.fr);
+    const int aoff = (c.wm * 128 + c.fr) * 64 + ((c.fq ^ sw) << 4);
+    const int boff = V12_A + (c.wn * 64 + c.fr) * 64 + ((c.fq ^ sw) << 4);
+    for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();
+        const char* st = smem + (kt & 1) * V12_STAGE;
+        char* ns = smem + ((kt + 1) & 1) * V12_STAGE;
+        if (kt + 1 < nk) {
+            const uint32_t koff = (uint32_t)(kt + 1) * 64;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dma(c.Ablk, oa[i] + koff, ns + (i * 4 + c.wid) * 1024);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) dma(c.Bblk, ob[i] + koff, ns + V12_A + (i * 4 + c.wid) * 1024);
+        }
+        bf16x8 a[8], b[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(st + aoff + i * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(st + boff + j * 1024);
+        mfma32(acc, a, b);
+    }
+    epilogue<G>(smem, acc, c, bias, C, M, N);
+}
+
 static void fill_bf16(std::vector<bf16_t>& v, float scale, unsigned seed) {
     std::mt19937 g(seed);
     std::uniform_real_distribution<float> d(-1.f, 1.f);
@@ -1091,7 +1206,9 @@ int main(int argc, char** argv) {
     Var vars[] = {{"V0", k_v01<false>}, {"V1", k_v01<true>}, {"V2", k_pp<false>}, {"V3", k_pp<true>},
                   {"V4r4", k_ring<4, false>}, {"V4r5", k_ring<5, false>}, {"V5r4", k_ring<4, true>},
                   {"V5r5", k_ring<5, true>}, {"V7", k_v7<false>}, {"V7p", k_v7<true>},
-                  {"V0samek", k_v01<false, true>}, {"V8", k_v8}, {"V9", k_v9}, {"V10", k_v10}, {"V11", k_v11}};
+                  {"V0samek", k_v01<false, true>}, {"V8", k_v8}, {"V9", k_v9}, {"V10", k_v10}, {"V11", k_v11},
+                  {"V0g1", k_v01<false, false, 1>}, {"V0g2", k_v01<false, false, 2>}, {"V12", k_v12<0>},
+                  {"V12g1", k_v12<1>}, {"V12g2", k_v12<2>}};
     const int NV = sizeof(vars) / sizeof(vars[0]);
     size_t maxA = 0, maxW = 0, maxC = 0;
     for (auto& s : shapes) {
@@ -1116,7 +1233,9 @@ int main(int argc, char** argv) {
         if (shape_filter[0] && !strstr(shape_filter, s.name)) continue;
         const int tiles = ((s.M + BM - 1) / BM) * ((s.N + BN - 1) / BN);
         const int tiles128 = ((s.M + BM - 1) / BM) * ((s.N + 127) / 128);
-        auto grid_of = [&](int v) { return dim3((strcmp(vars[v].name, "V9") == 0 || strcmp(vars[v].name, "V10") == 0) ? tiles128 : tiles); };
+        auto grid_of = [&](int v) { return dim3((strcmp(vars[v].name, "V9") == 0 || strcmp(vars[v].name, "V10") == 0 ||
+                                                  strncmp(vars[v].name, "V12", 3) == 0) ? tiles128 : tiles); };
+        auto block_of = [&](int v) { return dim3(strncmp(vars[v].name, "V12", 3) == 0 ? 256 : 512); };
         const double flop = 2.0 * s.M * (double)s.N * s.K;
         std::vector<std::vector<float>> ms(NV);
         auto on = [&](int v) { return !var_filter[0] || strstr(var_filter, vars[v].name); };
@@ -1127,7 +1246,7 @@ int main(int argc, char** argv) {
         CHECK(hipMemcpy(ref.data(), dC0, (size_t)s.M * s.N * 2, hipMemcpyDeviceToHost));
         for (int v = 1; v < NV; ++v) {
             CHECK(hipMemset(dC, 0, (size_t)s.M * s.N * 2));
-            hipLaunchKernelGGL(vars[v].f, grid_of(v), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
+            hipLaunchKernelGGL(vars[v].f, grid_of(v), block_of(v), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
             CHECK(hipDeviceSynchronize());
             CHECK(hipMemcpy(got.data(), dC, (size_t)s.M * s.N * 2, hipMemcpyDeviceToHost));
             size_t bad = 0;
@@ -1140,7 +1259,7 @@ int main(int argc, char** argv) {
                 if (!on(v)) { ms[v].push_back(0.f); continue; }
                 CHECK(hipEventRecord(e0, 0));
                 for (int it = 0; it < 3; ++it)
-                    hipLaunchKernelGGL(vars[v].f, grid_of(v), dim3(512), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
+                    hipLaunchKernelGGL(vars[v].f, grid_of(v), block_of(v), 0, 0, dA, dW, db, dC, s.M, s.N, s.K);
                 CHECK(hipEventRecord(e1, 0));
                 CHECK(hipEventSynchronize(e1));
                 float t; CHECK(hipEventElapsedTime(&t, e0, e1));

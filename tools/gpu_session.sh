@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU session: each GPU step under its own time limit; stop at the first crash / timeout / abort.
-# Usage: tools/gpu_session.sh <tag> [tests] [smoke] [bench] [prof]
+# Usage: tools/gpu_session.sh <tag> [tests] [smoke] [bench] [bench_np] [prof] [lab]
+#   env: PYTEST_K (pytest -k filter for "tests"), LAB_SHAPES / LAB_VARS (gemm_lab filters)
 TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
@@ -14,7 +15,7 @@ rocm-smi --showproductname > $OUT/gpu.txt 2>&1 || true
 for step in "$@"; do
   case $step in
     tests)
-      timeout -k 10 1500 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 -rf > $OUT/pytest_gpu.log 2>&1
+      timeout -k 10 1500 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 -rf ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1
       ok_or_stop $? tests; tail -30 $OUT/pytest_gpu.log ;;
     smoke)
       timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
@@ -29,6 +30,9 @@ for step in "$@"; do
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/prof.log 2>&1
       ok_or_stop $? prof; tail -3 $OUT/prof.log ;;
+    lab)
+      timeout -k 10 600 tools/gemm_lab/gemm_lab 5 "$LAB_SHAPES" "$LAB_VARS" 1 > $OUT/lab.log 2>&1
+      ok_or_stop $? lab; grep -v "inf TFLOP" $OUT/lab.log | tail -40 ;;
   esac
 done
 echo done | tee -a $OUT/status.txt

@@ -39,9 +39,13 @@ __device__ __forceinline__ bf16x4 ds_read_tr(const char* lds_base, int byte_off)
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_v4*>(p));
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // One key step of T 32-key tiles (T = 1 or 2) for a 32-query strip: S^T = K Q^T on MFMA, online softmax
-// update of (m, l, O), O^T += V^T P^T with V^T fragments from transposed LDS reads.
-template <int T>
+// update of (m, l, O), O^T += V^T P^T with V^T fragments from transposed LDS reads. MASK: this step contains
+// padded keys (only the last step). The O / l rescale is skipped when no query's running max moved in this
+// step (wave-uniform test), which is the common case after the first key tiles.
+template <int T, bool MASK>
 __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb, int N, int lane, const bf16x8 qf[4],
                                           float scale_log2, float& m, float& l, f32x16& o0, f32x16& o1) {
     const int l32 = lane & 31, hh = lane >> 5;
@@ -61,19 +65,27 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
     for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int key = kb + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const float v = key < N ? s[t][r] : -INFINITY;
-            s[t][r] = v;
-            bm = fmaxf(bm, v);
+            if constexpr (MASK) {
+                const int key = kb + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                if (key >= N) s[t][r] = -INFINITY;
+            }
+            bm = fmaxf(bm, s[t][r]);
         }
     bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-    const float mn = fmaxf(m, bm);
-    const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
-    m = mn;
-    const float msc = mn * scale_log2;
-    l *= alpha;
+    if (__builtin_expect(__any(bm > m), 0) || kb == 0) {
+        const float mn = fmaxf(m, bm);
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        m = mn;
+        l *= alpha;
+        const f32x2 a2 = {alpha, alpha};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+        for (int r = 0; r < 16; r += 2) {
+            f32x2 x0 = {o0[r], o0[r + 1]}, x1 = {o1[r], o1[r + 1]};
+            x0 *= a2; x1 *= a2;
+            o0[r] = x0.x; o0[r + 1] = x0.y; o1[r] = x1.x; o1[r + 1] = x1.y;
+        }
+    }
+    const float msc = m * scale_log2;
     bf16x8 pf[T][2];
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -111,7 +123,7 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
 }
 
 // One workgroup per (particle, head); one wave per 32-query strip (up to 8 waves, strips beyond loop).
-__global__ __launch_bounds__(512) void k_attn_bf16(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                    int N, int H, float scale_log2, int q_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int NP = (N + 31) & ~31;       // keys padded to whole 32-key MFMA tiles
@@ -150,9 +162,12 @@ __global__ __launch_bounds__(512) void k_attn_bf16(const bf16_t* __restrict__ qk
         }
         f32x16 o0 = {}, o1 = {};
         float m = -INFINITY, l = 0.f;
+        // full 32-key tiles need no mask; only the tail tile (NP - N padded keys) is masked. One S tile live
+        // keeps the kernel at <= 128 VGPRs = 4 waves/SIMD (two 7-wave workgroups per CU).
+        const int nfull = N & ~31;
         int kb = 0;
-        for (; kb + 64 <= NP; kb += 64) attn_step<2>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
-        if (kb < NP) attn_step<1>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+        for (; kb < nfull; kb += 32) attn_step<1, false>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+        if (kb < NP) attn_step<1, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
         l += __shfl_xor(l, 32, 64);
         const float inv = 1.0f / l;
         if (q < q_rows) {
