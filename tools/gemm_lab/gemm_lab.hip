@@ -17,6 +17,7 @@
 #include <cstring>
 #include <random>
 #include <vector>
+#include <type_traits>
 
 typedef unsigned short bf16_t;
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
@@ -350,6 +351,7 @@ template <int N> __device__ __forceinline__ void wait_vm() {
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 }
 __device__ __forceinline__ void wait_vm_rt(int n) {   // n = outstanding slices allowed (0..3)
     if (n >= 3) wait_vm<12>(); else if (n == 2) wait_vm<8>(); else if (n == 1) wait_vm<4>(); else wait_vm<0>();
@@ -1181,6 +1183,382 @@ __global__ __launch_bounds__(256, 2) void k_v12(const bf16_t* __restrict__ A, co
     epilogue<G>(smem, acc, c, bias, C, M, N);
 }
 
+
+// ---------------------------------------------------------------- V13: 4 waves x 128x128 (1 wave / SIMD)
+// hipBLASLt's gfx950 bf16 kernel shape (MT256x256x64, 256 threads, 130 KB LDS): each wave owns a 128x128
+// sub-tile (8 x 8 16x16x32 MFMA tiles, 256 fp32 accumulators in the unified VGPR/AGPR file), which halves
+// the LDS fragment reads per MFMA versus 8 waves of 128x64. Same 2-stage glds ring and swizzle as V0.
+template <int G = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_v13(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, const float* __restrict__ bias, bf16_t* C,
+           int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) char smem[LDSB];
+    const int wid0 = threadIdx.x >> 6;
+    Ctx c = make_ctx(A, W, M, N, K, wid0 >> 1, wid0 & 1);
+    uint32_t oa[8], ob[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        oa[i] = dma_off(i * 4 + c.wid, c.lane, M - 1 - c.m0, K);
+        ob[i] = dma_off(i * 4 + c.wid, c.lane, N - 1 - c.n0, K);
+    }
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = K / BK;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        dma(c.Ablk, oa[i], smem + (i * 4 + c.wid) * 1024);
+        dma(c.Bblk, ob[i], smem + OPB + (i * 4 + c.wid) * 1024);
+    }
+    const int sw = (c.fr >> 1) & 7;
+    for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();
+        const char* la = smem + (kt & 1) * STB;
+        const char* lb = la + OPB;
+        char* na = smem + ((kt + 1) & 1) * STB;
+        if (kt + 1 < nk) {
+            const uint32_t koff = (uint32_t)(kt + 1) * (BK * 2);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                dma(c.Ablk, oa[i] + koff, na + (i * 4 + c.wid) * 1024);
+                dma(c.Bblk, ob[i] + koff, na + OPB + (i * 4 + c.wid) * 1024);
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const char* pa = la + (c.wm * 128 + c.fr) * 128 + (((ks * 4 + c.fq) ^ sw) << 4);
+            const char* pb = lb + (c.wn * 128 + c.fr) * 128 + (((ks * 4 + c.fq) ^ sw) << 4);
+            bf16x8 a[8], b[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(pa + i * 2048);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) b[j] = *reinterpret_cast<const bf16x8*>(pb + j * 2048);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
+        }
+    }
+    // epilogue: two 128x64 halves per wave, 16 KiB image each (4 waves x 2 x 16 KiB = the whole ring)
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        char* img = smem + c.wid * 32768 + h * 16384;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ng = c.n0 + c.wn * 128 + h * 64 + j * 16 + c.fq * 4;
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = i * 16 + c.fr;
+                const int c8 = (j * 4 + c.fq) ^ (row & 15);
+                f32x2 v01 = {acc[h * 4 + j][i][0] + bv.x, acc[h * 4 + j][i][1] + bv.y};
+                f32x2 v23 = {acc[h * 4 + j][i][2] + bv.z, acc[h * 4 + j][i][3] + bv.w};
+                if constexpr (G == 1) { v01 = gelu_as26(v01); v23 = gelu_as26(v23); }
+                if constexpr (G == 2) { v01 = gelu_as28(v01); v23 = gelu_as28(v23); }
+                *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) = make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
+            }
+        }
+    }
+    __syncthreads();
+    const int c16 = c.lane & 7;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const char* img = smem + c.wid * 32768 + h * 16384;
+#pragma unroll 4
+        for (int it = 0; it < 16; ++it) {
+            const int row = it * 8 + (c.lane >> 3);
+            uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+            if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+            const int m = c.m0 + c.wm * 128 + row, n = c.n0 + c.wn * 128 + h * 64 + c16 * 8;
+            if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * N + n) = v;
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------- V14: V13 software-pipelined
+// 4 waves x 128x128, 4-slot ring of 32-deep slices (A 256 x 64 B + B 256 x 64 B = 32 KiB per slot, chunk
+// swizzle F = {0,2,3,1}). Iteration t: one barrier (slice t+1 landed for every wave; slot of slice t-1 free),
+// then 64 MFMAs on the fragments of slice t (registers) interleaved with the 16 fragment reads of slice t+1
+// and the 8 DMA pieces of slice t+3. DMA runs 3 slices (~3 K MFMA cycles) ahead; counted vmcnt.
+template <int G = 0, int INTERLEAVE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_v14(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, const float* __restrict__ bias, bf16_t* C,
+           int M, int N, int K) {
+    constexpr int SLOT = 32768;
+    __shared__ __attribute__((aligned(16))) char smem[4 * SLOT];
+    const int wid0 = threadIdx.x >> 6;
+    Ctx c = make_ctx(A, W, M, N, K, wid0 >> 1, wid0 & 1);
+    uint32_t oa[4], ob[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        oa[i] = dma_off32(i * 4 + c.wid, c.lane, M - 1 - c.m0, K);
+        ob[i] = dma_off32(i * 4 + c.wid, c.lane, N - 1 - c.n0, K);
+    }
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int ns = K / 32;
+    auto issue_piece = [&](int sl, int p) {       // p = 0..7: A pieces 0-3, B pieces 4-7
+        char* d = smem + (sl & 3) * SLOT;
+        const uint32_t koff = (uint32_t)sl * 64;
+        if (p < 4) dma(c.Ablk, oa[p] + koff, d + (p * 4 + c.wid) * 1024);
+        else dma(c.Bblk, ob[p - 4] + koff, d + 16384 + ((p - 4) * 4 + c.wid) * 1024);
+    };
+    const int sw = fsw(c.fr);
+    const int aoff = (c.wm * 128 + c.fr) * 64 + ((c.fq ^ sw) << 4);
+    const int boff = 16384 + (c.wn * 128 + c.fr) * 64 + ((c.fq ^ sw) << 4);
+    for (int sl = 0; sl < 3 && sl < ns; ++sl)
+#pragma unroll
+        for (int p = 0; p < 8; ++p) issue_piece(sl, p);
+    bf16x8 a0[8], b0[8], a1[8], b1[8];
+    if (ns >= 3) wait_vm<16>(); else if (ns == 2) wait_vm<8>(); else wait_vm<0>();
+    bar();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + aoff + i * 1024);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + boff + j * 1024);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    // Branch-free body (one basic block per slice, so the sched_group_barrier interleave applies): the
+    // fragment reads of "slice ns" read a stale slot (never used); DMA slices past the end re-fetch slice
+    // ns-1 into a slot nobody reads again; so every iteration waits vmcnt(8) (= the slice issued one
+    // iteration ago may still fly).
+    auto step = [&](int t, bf16x8 (&ac)[8], bf16x8 (&bc)[8], bf16x8 (&an)[8], bf16x8 (&bn)[8]) {
+        wait_vm<8>();
+        bar();
+        const char* ls = smem + ((t + 1) & 3) * SLOT;
+        char* dd = smem + ((t + 3) & 3) * SLOT;
+        const uint32_t koff = (uint32_t)min(t + 3, ns - 1) * 64;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], ac[i], acc[j][i], 0, 0, 0);
+            an[j] = *reinterpret_cast<const bf16x8*>(ls + aoff + j * 1024);
+            bn[j] = *reinterpret_cast<const bf16x8*>(ls + boff + j * 1024);
+            if (j < 4) dma(c.Ablk, oa[j] + koff, dd + (j * 4 + c.wid) * 1024);
+            else dma(c.Bblk, ob[j - 4] + koff, dd + 16384 + ((j - 4) * 4 + c.wid) * 1024);
+            if constexpr (INTERLEAVE) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    for (int t = 0; t < ns; t += 2) {
+        step(t, a0, b0, a1, b1);
+        step(t + 1, a1, b1, a0, b0);
+    }
+    // epilogue: two 128x64 halves per wave, 16 KiB image each (4 waves x 2 x 16 KiB = the whole ring)
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        char* img = smem + c.wid * 32768 + h * 16384;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ng = c.n0 + c.wn * 128 + h * 64 + j * 16 + c.fq * 4;
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ng < N) bv = *reinterpret_cast<const float4*>(bias + ng);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = i * 16 + c.fr;
+                const int c8 = (j * 4 + c.fq) ^ (row & 15);
+                f32x2 v01 = {acc[h * 4 + j][i][0] + bv.x, acc[h * 4 + j][i][1] + bv.y};
+                f32x2 v23 = {acc[h * 4 + j][i][2] + bv.z, acc[h * 4 + j][i][3] + bv.w};
+                if constexpr (G == 1) { v01 = gelu_as26(v01); v23 = gelu_as26(v23); }
+                if constexpr (G == 2) { v01 = gelu_as28(v01); v23 = gelu_as28(v23); }
+                *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) = make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
+            }
+        }
+    }
+    __syncthreads();
+    const int c16 = c.lane & 7;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const char* img = smem + c.wid * 32768 + h * 16384;
+#pragma unroll 4
+        for (int it = 0; it < 16; ++it) {
+            const int row = it * 8 + (c.lane >> 3);
+            uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+            if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+            const int m = c.m0 + c.wm * 128 + row, n = c.n0 + c.wn * 128 + h * 64 + c16 * 8;
+            if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * N + n) = v;
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------- V15: persistent V14
+// grid = min(tiles, CUs). Each workgroup walks tiles lid, lid + nwg, ... (XCD-grouped lid: the workgroups of
+// one XCD work on consecutive tiles). The slice stream is continuous across tiles: the DMA cursor runs 3
+// slices ahead and crosses into the next tile during the current tile's last slices, so no pipeline fill
+// per tile. DMA = buffer_load ... lds through a per-slice buffer resource (base = panel + k offset,
+// num_records = bytes left in the panel): rows past M / N are hardware OOB -> zeros, so per-lane offsets are
+// tile-invariant; a cursor past the last tile gets num_records = 0 (no traffic). First slice of a tile
+// runs its MFMAs with C = 0 (no accumulator reset). Epilogue stores 8-B pieces straight from the
+// accumulators; bias rides the DMA stream one tile ahead into a double-buffered LDS aux region.
+__device__ unsigned long long* g_dbg15;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void bdma(__amdgpu_buffer_rsrc_t r, uint32_t voff, char* lds) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+template <int G = 0, bool STAMP = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_v15(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, const float* __restrict__ bias, bf16_t* C,
+           int M, int N, int K) {
+    unsigned long long st_wait = 0, st_body = 0, st_epi = 0, st_t0 = 0;
+    constexpr int SLOT = 32768;
+    __shared__ __attribute__((aligned(16))) char smem[4 * SLOT + 2048];
+    char* aux = smem + 4 * SLOT;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid >> 1, wn = wid & 1, fr = lane & 15, fq = lane >> 4;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tiles_n = (N + 255) / 256, ntiles = ((M + 255) / 256) * tiles_n;
+    const int ns = K / 32;
+    uint32_t vo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = 16 * (i * 4 + wid) + (lane >> 2);
+        vo[i] = (uint32_t)row * (uint32_t)(K * 2) + (uint32_t)((((lane & 3) ^ fsw(row))) * 16);
+    }
+    // DMA cursor (wave-uniform)
+    int dtile = lid, dt = 0;
+    uint32_t dslot = 0;
+    auto dma_slice = [&]() {
+        const bool ok = dtile < ntiles;
+        const int tm = dtile / tiles_n, tn = dtile - tm * tiles_n;
+        const uint32_t ra = ok ? (uint32_t)min(M - tm * 256, 256) * (uint32_t)(K * 2) - (uint32_t)dt * 64 : 0u;
+        const uint32_t rb = ok ? (uint32_t)min(N - tn * 256, 256) * (uint32_t)(K * 2) - (uint32_t)dt * 64 : 0u;
+        const __amdgpu_buffer_rsrc_t rA = mk_rsrc(A + ((size_t)(ok ? tm : 0) * 256 * K + dt * 32), ra);
+        const __amdgpu_buffer_rsrc_t rB = mk_rsrc(W + ((size_t)(ok ? tn : 0) * 256 * K + dt * 32), rb);
+        char* d = smem + (dslot & 3) * SLOT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bdma(rA, vo[i], d + (i * 4 + wid) * 1024);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bdma(rB, vo[i], d + 16384 + (i * 4 + wid) * 1024);
+        ++dslot;
+        ++dt;
+        if (dt == ns) { dt = 0; dtile += nwg; }
+    };
+    auto dma_bias = [&](int tile, int buf) {   // wave 0 only
+        const bool ok = tile < ntiles;
+        const int tn = ok ? tile % tiles_n : 0;
+        const __amdgpu_buffer_rsrc_t rb = mk_rsrc(bias + tn * 256, ok ? (uint32_t)min(N - tn * 256, 256) * 4u : 0u);
+        bdma(rb, (uint32_t)lane * 16, aux + buf * 1024);
+    };
+    if (lid >= ntiles) return;
+    if (wid == 0) dma_bias(lid, 0);
+    dma_slice(); dma_slice(); dma_slice();
+    const int sw = fsw(fr);
+    const int aoff = (wm * 128 + fr) * 64 + ((fq ^ sw) << 4);
+    const int boff = 16384 + (wn * 128 + fr) * 64 + ((fq ^ sw) << 4);
+    bf16x8 a0[8], b0[8], a1[8], b1[8];
+    wait_vm<16>();
+    bar();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + aoff + i * 1024);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + boff + j * 1024);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    f32x4 acc[8][8];
+    uint32_t s = 0;   // global compute slice
+    auto step = [&](auto first, bf16x8 (&ac)[8], bf16x8 (&bc)[8], bf16x8 (&an)[8], bf16x8 (&bn)[8]) {
+        unsigned long long ta = 0, tb = 0;
+        if constexpr (STAMP) ta = __builtin_amdgcn_s_memtime();
+        wait_vm<8>();
+        bar();
+        if constexpr (STAMP) tb = __builtin_amdgcn_s_memtime();
+        const char* ls = smem + ((s + 1) & 3) * SLOT;
+        // the 8 DMA pieces of the cursor slice, spread over the 8 MFMA groups
+        const bool ok = dtile < ntiles;
+        const int tm = dtile / tiles_n, tn = dtile - tm * tiles_n;
+        const uint32_t ra = ok ? (uint32_t)min(M - tm * 256, 256) * (uint32_t)(K * 2) - (uint32_t)dt * 64 : 0u;
+        const uint32_t rb = ok ? (uint32_t)min(N - tn * 256, 256) * (uint32_t)(K * 2) - (uint32_t)dt * 64 : 0u;
+        const __amdgpu_buffer_rsrc_t rA = mk_rsrc(A + ((size_t)(ok ? tm : 0) * 256 * K + dt * 32), ra);
+        const __amdgpu_buffer_rsrc_t rB = mk_rsrc(W + ((size_t)(ok ? tn : 0) * 256 * K + dt * 32), rb);
+        char* dd = smem + (dslot & 3) * SLOT;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if constexpr (decltype(first)::value)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], ac[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                else
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], ac[i], acc[j][i], 0, 0, 0);
+            }
+            an[j] = *reinterpret_cast<const bf16x8*>(ls + aoff + j * 1024);
+            bn[j] = *reinterpret_cast<const bf16x8*>(ls + boff + j * 1024);
+            if (j < 4) bdma(rA, vo[j], dd + (j * 4 + wid) * 1024);
+            else bdma(rB, vo[j - 4], dd + 16384 + ((j - 4) * 4 + wid) * 1024);
+            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        ++dslot;
+        ++dt;
+        if (dt == ns) { dt = 0; dtile += nwg; }
+        ++s;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (STAMP) { const unsigned long long tc = __builtin_amdgcn_s_memtime(); st_wait += tb - ta; st_body += tc - tb; }
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    int k = 0;
+    for (int tile = lid; tile < ntiles; tile += nwg, ++k) {
+        step(T{}, a0, b0, a1, b1);
+        step(F{}, a1, b1, a0, b0);
+        for (int t = 2; t < ns; t += 2) {
+            step(F{}, a0, b0, a1, b1);
+            step(F{}, a1, b1, a0, b0);
+        }
+        unsigned long long te0 = 0;
+        if constexpr (STAMP) te0 = __builtin_amdgcn_s_memtime();
+        // next tile's bias (lands long before its epilogue; older than the slices waited on -> counted)
+        if (wid == 0) dma_bias(tile + nwg, (k + 1) & 1);
+        // epilogue of this tile, straight from the accumulators
+        const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+        const char* ab = aux + (k & 1) * 1024;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int nl = wn * 128 + j * 16 + fq * 4;
+            const float4 bv = *reinterpret_cast<const float4*>(ab + nl * 4);
+            const int n = tn * 256 + nl;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int m = tm * 256 + wm * 128 + i * 16 + fr;
+                f32x2 v01 = {acc[j][i][0] + bv.x, acc[j][i][1] + bv.y};
+                f32x2 v23 = {acc[j][i][2] + bv.z, acc[j][i][3] + bv.w};
+                if constexpr (G == 1) { v01 = gelu_as26(v01); v23 = gelu_as26(v23); }
+                if constexpr (G == 2) { v01 = gelu_as28(v01); v23 = gelu_as28(v23); }
+                if (m < M && n < N)
+                    *reinterpret_cast<uint2*>(C + (int64_t)m * N + n) = make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
+            }
+        }
+        if constexpr (STAMP) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); st_epi += __builtin_amdgcn_s_memtime() - te0; }
+    }
+    if constexpr (STAMP) {
+        if (lane == 0) {
+            unsigned long long* o = g_dbg15 + ((size_t)blockIdx.x * 4 + wid) * 4;
+            o[0] = st_wait; o[1] = st_body; o[2] = st_epi; o[3] = (unsigned long long)k;
+        }
+    }
+    wait_vm<0>();   // outstanding (OOB / zero) DMAs must land before the workgroup's LDS is released
+}
+
 static void fill_bf16(std::vector<bf16_t>& v, float scale, unsigned seed) {
     std::mt19937 g(seed);
     std::uniform_real_distribution<float> d(-1.f, 1.f);
@@ -1208,7 +1586,10 @@ int main(int argc, char** argv) {
                   {"V5r5", k_ring<5, true>}, {"V7", k_v7<false>}, {"V7p", k_v7<true>},
                   {"V0samek", k_v01<false, true>}, {"V8", k_v8}, {"V9", k_v9}, {"V10", k_v10}, {"V11", k_v11},
                   {"V0g1", k_v01<false, false, 1>}, {"V0g2", k_v01<false, false, 2>}, {"V12", k_v12<0>},
-                  {"V12g1", k_v12<1>}, {"V12g2", k_v12<2>}};
+                  {"V12g1", k_v12<1>}, {"V12g2", k_v12<2>},
+                  {"V13", k_v13<0>}, {"V13g2", k_v13<2>},
+                  {"V14", k_v14<0, 1>}, {"V14n", k_v14<0, 0>}, {"V14g2", k_v14<2, 1>},
+                  {"V15", k_v15<0>}, {"V15g2", k_v15<2>}};
     const int NV = sizeof(vars) / sizeof(vars[0]);
     size_t maxA = 0, maxW = 0, maxC = 0;
     for (auto& s : shapes) {
@@ -1234,8 +1615,11 @@ int main(int argc, char** argv) {
         const int tiles = ((s.M + BM - 1) / BM) * ((s.N + BN - 1) / BN);
         const int tiles128 = ((s.M + BM - 1) / BM) * ((s.N + 127) / 128);
         auto grid_of = [&](int v) { return dim3((strcmp(vars[v].name, "V9") == 0 || strcmp(vars[v].name, "V10") == 0 ||
-                                                  strncmp(vars[v].name, "V12", 3) == 0) ? tiles128 : tiles); };
-        auto block_of = [&](int v) { return dim3(strncmp(vars[v].name, "V12", 3) == 0 ? 256 : 512); };
+                                                  strncmp(vars[v].name, "V12", 3) == 0) ? tiles128
+                                               : strncmp(vars[v].name, "V15", 3) == 0 ? std::min(tiles, 256) : tiles); };
+        auto block_of = [&](int v) { return dim3(strncmp(vars[v].name, "V12", 3) == 0 || strncmp(vars[v].name, "V13", 3) == 0 ||
+                                                          strncmp(vars[v].name, "V14", 3) == 0 ||
+                                                          strncmp(vars[v].name, "V15", 3) == 0 ? 256 : 512); };
         const double flop = 2.0 * s.M * (double)s.N * s.K;
         std::vector<std::vector<float>> ms(NV);
         auto on = [&](int v) { return !var_filter[0] || strstr(var_filter, vars[v].name); };
@@ -1272,6 +1656,27 @@ int main(int argc, char** argv) {
                    s.K, med, flop / (med * 1e-3) / 1e12, ms[v][0]);
         }
         fflush(stdout);
+    }
+    if (getenv("LAB_STAMPS15")) {
+        for (auto& sh : shapes) {
+            if (shape_filter[0] && !strstr(shape_filter, sh.name)) continue;
+            const int tiles = ((sh.M + 255) / 256) * ((sh.N + 255) / 256);
+            const int g = std::min(tiles, 256);
+            unsigned long long* dbg;
+            CHECK(hipMalloc(&dbg, (size_t)g * 16 * 8));
+            CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg15), &dbg, sizeof(dbg)));
+            for (int rep = 0; rep < 2; ++rep)
+                hipLaunchKernelGGL((k_v15<0, true>), dim3(g), dim3(256), 0, 0, dA, dW, db, dC, sh.M, sh.N, sh.K);
+            CHECK(hipDeviceSynchronize());
+            std::vector<unsigned long long> h((size_t)g * 16);
+            CHECK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+            double w = 0, b = 0, e = 0, nt = 0;
+            for (int i = 0; i < g * 4; ++i) { w += h[i * 4]; b += h[i * 4 + 1]; e += h[i * 4 + 2]; nt += h[i * 4 + 3]; }
+            const double slices = nt * (sh.K / 32);
+            printf("V15 stamps %s: per slice wait+bar %.0f body %.0f | per tile epilogue %.0f (memtime units; tiles/wave %.1f)\n",
+                   sh.name, w / slices, b / slices, e / nt, nt / (g * 4));
+            CHECK(hipFree(dbg));
+        }
     }
     if (getenv("LAB_STAMPS10")) {
         for (auto& s : shapes) {
