@@ -75,7 +75,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                                                         const float* __restrict__ pos, int g2,
                                                         const float2* __restrict__ stats,
                                                         const float* __restrict__ colsum,
-                                                        bf16_t* C, int ldc, int M, int N, int K) {
+                                                        bf16_t* C, int ldc, int M, int N, int K, int group) {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES + AUX_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -84,8 +84,24 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    // Grouped order inside each XCD's contiguous lid range: groups of `group` A row-panels; within a group
+    // the A panel index runs fastest, so the ~32 tiles an XCD has in flight cover ~group A panels x
+    // 32/group W panels and both stay in that XCD's L2 (tm-major order re-fetched a 393 KB W panel per
+    // tile on FC1: FETCH_SIZE 14.8 GB/launch, profiles/r1_notes.md). group = 0: plain tm-major.
     const int tiles_n = (N + BN - 1) / BN;
-    const int tm = lid / tiles_n, tn = lid - (lid / tiles_n) * tiles_n;
+    int tm, tn;
+    if (group > 0) {
+        const int tiles_m = (M + BM - 1) / BM;
+        const int per_group = group * tiles_n;
+        const int g = lid / per_group, idx = lid - g * per_group;
+        const int gm0 = g * group;
+        const int gsz = min(group, tiles_m - gm0);
+        tn = idx / gsz;
+        tm = gm0 + (idx - tn * gsz);
+    } else {
+        tm = lid / tiles_n;
+        tn = lid - tm * tiles_n;
+    }
     const int m0 = tm * BM, n0 = tn * BN;
 
     // ---- per-lane DMA source offsets (bytes, relative to the block's panel base) ----
@@ -489,7 +505,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16_pers(const bf16_t* __res
                                k, (int)tiles);                                                               \
         else                                                                                                 \
             hipLaunchKernelGGL(k_gemm_bf16<E>, grid, block, 0, s, A, (int)lda, W, bias, residual, pos, patch_rows, \
-                               reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k);    \
+                               reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k, group); \
     } while (0)
 
 // VPF_GEMM_PERSISTENT=1 selects the persistent kernel (one workgroup per CU); the default is one tile per
@@ -504,6 +520,12 @@ static int cu_count() {
     }
     return cached;
 }
+static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size of the tile order (0 = tm-major)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("VPF_GEMM_GROUP"); v = e ? atoi(e) : 8; if (v < 0) v = 0; }
+    return v;
+}
+
 static bool use_persistent() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("VPF_GEMM_PERSISTENT"); v = (e && e[0] == '1') ? 1 : 0; }
@@ -530,6 +552,7 @@ VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, con
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)tiles), block(NTHREADS);
     const bool pers = use_persistent();
+    const int group = tile_group();
     const dim3 pgrid((unsigned)(tiles < cu_count() ? tiles : cu_count()));
     const int m = (int)M, n = (int)N, k = (int)K;
     switch (epilogue) {
