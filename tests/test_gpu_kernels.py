@@ -251,6 +251,54 @@ def test_attention_q_rows(dtype):
     assert torch.all(part[:, 1:] == 5.0)
 
 
+@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("B,N,H", [(100, 197, 12), (90, 256, 12), (96, 280, 12)])
+def test_attention_bf16_large(B, N, H, mode, monkeypatch):
+    """B*H >= 4 x CUs. mode "1" selects the persistent double-buffered kernel (VPF_ATTN_MODE); N = 280 has 9
+    query strips, so a wave also takes a second strip. Both kernels must agree bit for bit."""
+    torch.manual_seed(N + H)
+    D = 64 * H
+    qkv = (torch.randn(B, N, 3 * D, device=DEV) * 1.5).to(torch.bfloat16)
+    monkeypatch.setenv("VPF_ATTN_MODE", "0")
+    base = torch.empty(B, N, D, device=DEV, dtype=torch.bfloat16)
+    vpf().attention(qkv, H, N, base)
+    monkeypatch.setenv("VPF_ATTN_MODE", mode)
+    out = torch.empty(B, N, D, device=DEV, dtype=torch.bfloat16)
+    vpf().attention(qkv, H, N, out)
+    assert torch.equal(out, base)
+    q, k, v = qkv.float().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = torch.softmax((q @ k.transpose(-1, -2)) * 0.125, -1) @ v
+    ref = ref.transpose(1, 2).reshape(B, N, D)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    part = torch.full((B, N, D), 5.0, device=DEV, dtype=torch.bfloat16)
+    vpf().attention(qkv, H, 1, part)
+    assert torch.equal(part[:, 0], out[:, 0])
+    assert torch.all(part[:, 1:] == 5.0)
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_attention_bf16_rescale_branch(mode, monkeypatch):
+    """The lazy online-softmax rescale only runs when a query's max grows by > 2^8 (exp2 domain) within a
+    key tile: force it (a key row aligned with a query, late in the sequence) and also plant spikes below the
+    threshold, then check against a full fp64 reference (cdna_hip_programming.md §5.4 rule 26)."""
+    torch.manual_seed(26)
+    B, N, H = 100, 197, 12
+    D = 64 * H
+    qkv = (torch.randn(B, N, 3 * D, device=DEV) * 0.5).to(torch.bfloat16)
+    for b in range(0, B, 7):
+        h = b % H
+        q = qkv[b, 5, h * 64:(h + 1) * 64].float()
+        qkv[b, 150, D + h * 64:D + (h + 1) * 64] = (q * 12.0).to(torch.bfloat16)       # far past the threshold
+        qkv[b, 40, D + h * 64:D + (h + 1) * 64] = (q * 1.5).to(torch.bfloat16)         # moderate, below it
+        qkv[b, 196, D + h * 64:D + (h + 1) * 64] = (q * 20.0).to(torch.bfloat16)       # in the masked tail tile
+    monkeypatch.setenv("VPF_ATTN_MODE", mode)
+    out = torch.empty(B, N, D, device=DEV, dtype=torch.bfloat16)
+    vpf().attention(qkv, H, N, out)
+    q, k, v = qkv.double().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax((q @ k.transpose(-1, -2)) * 0.125, -1) @ v).transpose(1, 2).reshape(B, N, D)
+    torch.testing.assert_close(out.double(), ref, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("B,N,H", [(2, 197, 3), (1, 50, 2)])
 def test_attention_f32(B, N, H):
     torch.manual_seed(N)

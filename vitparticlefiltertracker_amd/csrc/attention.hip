@@ -15,6 +15,8 @@
 //
 // fp32 parity path (vpf_attention_f32): one thread per query, K/V of the head in LDS as fp32, exact
 // expf softmax (N <= 256).
+#include <cstdlib>
+
 #include "vpf_common.h"
 #include "../../include/vpf.h"
 
@@ -25,6 +27,9 @@ typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
 
 constexpr int HD = 64;
 constexpr int ROWB = HD * 2;  // 128 B per K/V row
@@ -72,17 +77,18 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
             bm = fmaxf(bm, s[t][r]);
         }
     bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-    if (__builtin_expect(__any(bm > m), 0) || kb == 0) {
+    // Lazy rescale (T13): the running max m only moves when some query's tile max exceeds it by more than
+    // 8 in the exp2 domain, so probabilities stay <= 2^8 (exact in fp32 accumulation, representable in bf16)
+    // and the O / l rescale is skipped on almost every tile. The first tile always sets m (m = -inf).
+    if (__builtin_expect(__any((bm - m) * scale_log2 > 8.0f), 0)) {
         const float mn = fmaxf(m, bm);
         const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
         m = mn;
         l *= alpha;
-        const f32x2 a2 = {alpha, alpha};
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-            f32x2 x0 = {o0[r], o0[r + 1]}, x1 = {o1[r], o1[r + 1]};
-            x0 *= a2; x1 *= a2;
-            o0[r] = x0.x; o0[r + 1] = x0.y; o1[r] = x1.x; o1[r + 1] = x1.y;
+        for (int r = 0; r < 16; ++r) {
+            o0[r] *= alpha;
+            o1[r] *= alpha;
         }
     }
     const float msc = m * scale_log2;
@@ -138,27 +144,40 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const bf16_t* vbase = qbase + 2 * D;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
 
-    for (int idx = tid; idx < NP * 8; idx += blockDim.x) {
-        const int r = idx >> 3, c = idx & 7;
-        uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-        if (r < N) {
-            kv = *reinterpret_cast<const uint4*>(kbase + (int64_t)r * 3 * D + c * 8);
-            vv = *reinterpret_cast<const uint4*>(vbase + (int64_t)r * 3 * D + c * 8);
+    // K/V staging: every DMA piece (8 rows x 128 B per wave-instruction, swizzle applied on the source
+    // address, lane-linear LDS destination) is in flight at once, and the first strip's Q loads are issued
+    // under it. Rows >= N are filled from row N-1: finite values whose keys are masked (probability 0).
+    {
+        const int ninstr = NP >> 3, sub = lane >> 3, slot = lane & 7;
+        for (int j = wid; j < 2 * ninstr; j += nw) {
+            const bool isv = j >= ninstr;
+            const int g = isv ? j - ninstr : j;
+            const int r = 8 * g + sub;
+            const int c = isv ? (slot ^ (((r >> 1) & 1) << 2)) : (slot ^ ((r >> 1) & 7));
+            const bf16_t* src = (isv ? vbase : kbase) + (int64_t)min(r, N - 1) * 3 * D + c * 8;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)((isv ? Vs : Ks) + g * 1024), 16, 0, 0);
         }
-        *reinterpret_cast<uint4*>(Ks + k_off(r, c)) = kv;
-        *reinterpret_cast<uint4*>(Vs + v_off(r, c)) = vv;
+    }
+    const int l32 = lane & 31, hh = lane >> 5;
+    const int nstrips = (q_rows + 31) >> 5;
+    bf16x8 q0[4];
+    {
+        const int q = min(wid * 32 + l32, N - 1);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) q0[ks] = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)q * 3 * D + ks * 16 + hh * 8);
     }
     __syncthreads();
 
-    const int l32 = lane & 31, hh = lane >> 5;
-    const int nstrips = (q_rows + 31) >> 5;
     for (int strip = wid; strip < nstrips; strip += nw) {
         const int q = strip * 32 + l32;
         bf16x8 qf[4];
+        if (strip == wid) {
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            if (q < N) qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)q * 3 * D + ks * 16 + hh * 8);
-            else qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            for (int ks = 0; ks < 4; ++ks) qf[ks] = q0[ks];
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+                qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)min(q, N - 1) * 3 * D + ks * 16 + hh * 8);
         }
         f32x16 o0 = {}, o1 = {};
         float m = -INFINITY, l = 0.f;
@@ -182,6 +201,119 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             }
         }
     }
+}
+
+
+// Persistent variant (N <= 312, i.e. two K/V images fit in LDS): one 512-thread workgroup per CU walks
+// (particle, head) pairs bh = blockIdx.x, + gridDim.x, ... K/V of the next pair are DMA'd
+// (global_load_lds, 16 B per lane, swizzle on the source address) into the other half of a double-buffered
+// LDS image while the current pair computes, and the next pair's Q fragments are prefetched into registers,
+// so HBM streaming overlaps the MFMA/softmax work instead of alternating with it. A pair's output is stored
+// after the barrier that ends it, so the per-pair vmcnt(0) (which retires the next pair's DMA) never waits
+// on fresh stores. Rows >= N of the images are filled from row N-1 (finite values; their keys are masked
+// and their probabilities are exactly 0).
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+void k_attn_bf16_pers(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, int BH,
+                      float scale_log2, int q_rows) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int NP = (N + 31) & ~31;
+    const int IMG = NP * ROWB;            // one K or V image
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int D = H * HD;
+    const int l32 = lane & 31, hh = lane >> 5;
+    const int nstrips = (q_rows + 31) >> 5;
+    const int ninstr = NP >> 3;           // 8 rows (1 KiB) per DMA wave-instruction, per image
+    const int sub = lane >> 3, slot = lane & 7;
+
+    auto issue_kv = [&](int bh, int buf) {
+        const int b = bh / H, h = bh - (bh / H) * H;
+        const bf16_t* base = qkv + (int64_t)b * N * 3 * D + h * HD;
+        char* kimg = smem + buf * 2 * IMG;
+        char* vimg = kimg + IMG;
+        for (int j = wid; j < 2 * ninstr; j += 8) {
+            const bool isv = j >= ninstr;
+            const int g = isv ? j - ninstr : j;
+            const int r = 8 * g + sub;
+            const int c = isv ? (slot ^ (((r >> 1) & 1) << 2)) : (slot ^ ((r >> 1) & 7));
+            const bf16_t* src = base + (int64_t)min(r, N - 1) * 3 * D + (isv ? 2 * D : D) + c * 8;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)((isv ? vimg : kimg) + g * 1024), 16, 0, 0);
+        }
+    };
+    auto load_q = [&](int bh, int strip, bf16x8 (&qf)[4]) {
+        const int b = bh / H, h = bh - (bh / H) * H;
+        const int q = strip * 32 + l32;
+        const bf16_t* qb = qkv + ((int64_t)b * N + min(q, N - 1)) * 3 * D + h * HD + hh * 8;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qb + ks * 16);
+    };
+    auto store_o = [&](int bh, int strip, const f32x16& o0, const f32x16& o1, float l) {
+        const int q = strip * 32 + l32;
+        if (q >= q_rows) return;
+        const int b = bh / H, h = bh - (bh / H) * H;
+        const float inv = 1.0f / l;
+        bf16_t* orow = out + ((int64_t)b * N + q) * D + h * HD;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d = 8 * g4 + 4 * hh;
+            *reinterpret_cast<uint2*>(orow + d) =
+                make_uint2(pack_bf2(o0[4 * g4] * inv, o0[4 * g4 + 1] * inv), pack_bf2(o0[4 * g4 + 2] * inv, o0[4 * g4 + 3] * inv));
+            *reinterpret_cast<uint2*>(orow + 32 + d) =
+                make_uint2(pack_bf2(o1[4 * g4] * inv, o1[4 * g4 + 1] * inv), pack_bf2(o1[4 * g4 + 2] * inv, o1[4 * g4 + 3] * inv));
+        }
+    };
+
+    int bh = blockIdx.x;
+    if (bh >= BH) return;
+    const bool has_strip = wid < nstrips;
+    bf16x8 qn[4];
+    issue_kv(bh, 0);
+    if (has_strip) load_q(bh, wid, qn);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    f32x16 o0 = {}, o1 = {};
+    float l = 1.f;
+    int prev = -1;
+    for (int it = 0; bh < BH; ++it, bh += gridDim.x) {
+        const int buf = it & 1;
+        const int nbh = bh + gridDim.x;
+        if (prev >= 0 && has_strip) store_o(prev, wid, o0, o1, l);     // previous pair's strip
+        if (nbh < BH) issue_kv(nbh, buf ^ 1);
+        bf16x8 qf[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = qn[ks];
+        if (nbh < BH && has_strip) load_q(nbh, wid, qn);
+        const char* Ks = smem + buf * 2 * IMG;
+        const char* Vs = Ks + IMG;
+        const int nfull = N & ~31;
+        // extra strips (N > 256) first, stored at once; the wave's own strip last, so its accumulators are the
+        // ones kept for the deferred store after the barrier
+        int last = wid;
+        while (last + 8 < nstrips) last += 8;
+        for (int strip = last; strip >= wid && strip < nstrips; strip -= 8) {
+            bf16x8 qs[4];
+            if (strip != wid) {
+                load_q(bh, strip, qs);
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) qs[ks] = qf[ks];
+            }
+            o0 = f32x16{};
+            o1 = f32x16{};
+            float m = -INFINITY;
+            l = 0.f;
+            int kb = 0;
+            for (; kb < nfull; kb += 32) attn_step<1, false>(Ks, Vs, kb, N, lane, qs, scale_log2, m, l, o0, o1);
+            if (kb < NP) attn_step<1, true>(Ks, Vs, kb, N, lane, qs, scale_log2, m, l, o0, o1);
+            l += __shfl_xor(l, 32, 64);
+            if (strip != wid) store_o(bh, strip, o0, o1, l);
+        }
+        prev = bh;
+        // retires the next pair's K/V DMA and Q prefetch (issued one pair ago) and the stores of the pair before
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (has_strip) store_o(prev, wid, o0, o1, l);
 }
 
 // ---------------- fp32 parity path ----------------
@@ -227,6 +359,18 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ qkv,
 
 }  // namespace
 
+static int cu_count() {
+    static int cached = 0;
+    if (!cached) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cached = n;
+        else
+            cached = 256;
+    }
+    return cached;
+}
+
 VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd, float scale,
                                int q_rows, void* stream) {
     if (B < 0 || N <= 0 || N > 640 || H <= 0 || hd != HD || B * H > INT32_MAX || q_rows < 1 || q_rows > N)
@@ -236,6 +380,20 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     const size_t lds = (size_t)NP * ROWB * 2;
     const float scale_log2 = scale * 1.44269504088896341f;
     const int strips = (q_rows + 31) / 32;
+    const int64_t BH = B * H;
+    const char* mode = getenv("VPF_ATTN_MODE");   // "1": persistent double-buffered kernel (design aid)
+    if (mode && mode[0] == '1' && 2 * lds <= 150 * 1024 && BH >= 4 * cu_count()) {
+        static bool pattr = false;   // benign race: idempotent attribute set
+        if (!pattr) {
+            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pers, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024);
+            pattr = true;
+        }
+        const int grid = cu_count();
+        hipLaunchKernelGGL(k_attn_bf16_pers, dim3((unsigned)grid), dim3(512), 2 * lds, (hipStream_t)stream, qkv, out,
+                           N, H, (int)BH, scale_log2, q_rows);
+        VPF_RETURN_LAUNCH();
+    }
     const int threads = 64 * (strips < 8 ? strips : 8);
     static bool attr_set = false;   // benign race: idempotent attribute set
     if (!attr_set) {

@@ -22,9 +22,12 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
     __bf16 b = (__bf16)f;
     return __builtin_bit_cast(bf16_t, b);
 }
-// two floats -> packed bf16x2 (lo in bits 0..15)
+// two floats -> packed bf16x2 (lo in bits 0..15), round-to-nearest-even: ONE v_cvt_pk_bf16_f32 (two scalar
+// casts + shift/or cost four VALU instructions).
+typedef __bf16 vpf_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float vpf_f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-    return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(vpf_f32x2{lo, hi}, vpf_bf16x2));
 }
 
 // ---------------- Philox4x32-10 (SPEC S1) ----------------
