@@ -93,7 +93,7 @@ int vpf_layernorm_f32(const float* x, int64_t rows, int D, int64_t x_stride, con
 
 /* H6: per (particle, head) softmax(q k^T * scale) v. qkv: [B][N][3][H][hd], out: [B][N][H][hd].
  * Only the first q_rows queries of every particle are computed (q_rows = N: all; 1: the CLS row, used by
- * the last encoder layer whose other rows feed nothing). hd == 64, N <= 640 (f32: N <= 256). */
+ * the last encoder layer whose other rows feed nothing). hd == 64, N <= 640 (f32: N <= 4096, keys streamed through LDS in 128-key chunks). */
 int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd,
                        float scale, int q_rows, void* stream);
 int vpf_attention_f32(const float* qkv, float* out, int64_t B, int N, int H, int hd, float scale,

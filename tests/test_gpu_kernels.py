@@ -299,7 +299,7 @@ def test_attention_bf16_rescale_branch(mode, monkeypatch):
     torch.testing.assert_close(out.double(), ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("B,N,H", [(2, 197, 3), (1, 50, 2)])
+@pytest.mark.parametrize("B,N,H", [(2, 197, 3), (1, 50, 2), (1, 577, 2)])
 def test_attention_f32(B, N, H):
     torch.manual_seed(N)
     D = 64 * H

@@ -30,7 +30,8 @@ def _crops(arch, n, seed=0):
 
 
 @pytest.mark.parametrize("name,dtype,n", [("vit_tiny_patch16_224", "fp32", 5), ("vit_tiny_patch16_224", "bf16", 9),
-                                          ("vit_base_patch16_224", "bf16", 3), ("vit_base_patch16_224", "fp32", 2)])
+                                          ("vit_base_patch16_224", "bf16", 3), ("vit_base_patch16_224", "fp32", 2),
+                                          ("vit_large_patch14_336", "bf16", 2), ("vit_large_patch14_336", "fp32", 1)])
 def test_vit_features_vs_oracle(name, dtype, n):
     from vitparticlefiltertracker_amd.vit import ViTEngine
     arch = ARCHS[name]

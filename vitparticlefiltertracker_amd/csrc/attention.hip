@@ -317,43 +317,64 @@ void k_attn_bf16_pers(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, 
 }
 
 // ---------------- fp32 parity path ----------------
+// One thread per query; K / V of the (particle, head) stream through LDS in chunks of KC keys, so any N
+// works (ViT-L/14 @ 336: N = 577). Exact two-pass softmax in key order: pass 1 the row max over all keys,
+// pass 2 p = expf(s*scale - max), l += p, acc += p v.
+constexpr int KC = 128;
 __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ qkv, float* __restrict__ out, int N,
                                                   int H, float scale, int q_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* Ks = reinterpret_cast<float*>(smem);
-    float* Vs = Ks + N * HD;
+    float* Vs = Ks + KC * HD;
     const int bh = blockIdx.x;
     const int b = bh / H, h = bh - (bh / H) * H;
     const int D = H * HD;
     const int64_t row0 = (int64_t)b * N;
     const float* qbase = qkv + row0 * 3 * D + h * HD;
-    for (int idx = threadIdx.x; idx < N * HD; idx += blockDim.x) {
-        const int r = idx / HD, c = idx - (idx / HD) * HD;
-        Ks[idx] = qbase[(int64_t)r * 3 * D + D + c];
-        Vs[idx] = qbase[(int64_t)r * 3 * D + 2 * D + c];
-    }
-    __syncthreads();
-    for (int q = threadIdx.x; q < q_rows; q += blockDim.x) {
+    auto stage = [&](int c0, bool with_v) {
+        const int rows = min(KC, N - c0);
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < rows * HD; idx += blockDim.x) {
+            const int r = idx / HD, c = idx - (idx / HD) * HD;
+            Ks[idx] = qbase[(int64_t)(c0 + r) * 3 * D + D + c];
+            if (with_v) Vs[idx] = qbase[(int64_t)(c0 + r) * 3 * D + 2 * D + c];
+        }
+        __syncthreads();
+        return rows;
+    };
+    for (int q0 = 0; q0 < q_rows; q0 += blockDim.x) {
+        const int q = q0 + threadIdx.x;
+        const bool active = q < q_rows;
         float qv[HD];
-        for (int c = 0; c < HD; ++c) qv[c] = qbase[(int64_t)q * 3 * D + c];
+        for (int c = 0; c < HD; ++c) qv[c] = active ? qbase[(int64_t)q * 3 * D + c] : 0.f;
         float mx = -INFINITY;
-        for (int k = 0; k < N; ++k) {
-            float s = 0.f;
-            for (int c = 0; c < HD; ++c) s = fmaf(qv[c], Ks[k * HD + c], s);
-            mx = fmaxf(mx, s * scale);
+        for (int c0 = 0; c0 < N; c0 += KC) {
+            const int rows = stage(c0, false);
+            if (active)
+                for (int k = 0; k < rows; ++k) {
+                    float s = 0.f;
+                    for (int c = 0; c < HD; ++c) s = fmaf(qv[c], Ks[k * HD + c], s);
+                    mx = fmaxf(mx, s * scale);
+                }
         }
         float acc[HD];
         for (int c = 0; c < HD; ++c) acc[c] = 0.f;
         float l = 0.f;
-        for (int k = 0; k < N; ++k) {
-            float s = 0.f;
-            for (int c = 0; c < HD; ++c) s = fmaf(qv[c], Ks[k * HD + c], s);
-            const float p = expf(s * scale - mx);
-            l += p;
-            for (int c = 0; c < HD; ++c) acc[c] = fmaf(p, Vs[k * HD + c], acc[c]);
+        for (int c0 = 0; c0 < N; c0 += KC) {
+            const int rows = stage(c0, true);
+            if (active)
+                for (int k = 0; k < rows; ++k) {
+                    float s = 0.f;
+                    for (int c = 0; c < HD; ++c) s = fmaf(qv[c], Ks[k * HD + c], s);
+                    const float p = expf(s * scale - mx);
+                    l += p;
+                    for (int c = 0; c < HD; ++c) acc[c] = fmaf(p, Vs[k * HD + c], acc[c]);
+                }
         }
-        float* orow = out + (row0 + q) * D + h * HD;
-        for (int c = 0; c < HD; ++c) orow[c] = acc[c] / l;
+        if (active) {
+            float* orow = out + (row0 + q) * D + h * HD;
+            for (int c = 0; c < HD; ++c) orow[c] = acc[c] / l;
+        }
     }
 }
 
@@ -407,10 +428,10 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
 
 VPF_API int vpf_attention_f32(const float* qkv, float* out, int64_t B, int N, int H, int hd, float scale,
                               int q_rows, void* stream) {
-    if (B < 0 || N <= 0 || N > 256 || H <= 0 || hd != HD || B * H > INT32_MAX || q_rows < 1 || q_rows > N)
+    if (B < 0 || N <= 0 || N > 4096 || H <= 0 || hd != HD || B * H > INT32_MAX || q_rows < 1 || q_rows > N)
         return VPF_ERR_ARG;
     if (B == 0) return 0;
-    const size_t lds = (size_t)N * HD * 4 * 2;
+    const size_t lds = (size_t)KC * HD * 4 * 2;   // one K chunk + one V chunk
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_attn_f32, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
