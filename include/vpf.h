@@ -46,13 +46,14 @@ int vpf_predict(float* particles, int64_t n, int64_t ld, int64_t global_begin, u
                 float smin, float smax, void* stream);
 
 /* H2+H3 (A operand of the patch embed): bilinear crop + normalise + im2col, SPEC S3.
- * frame: uint8[H][W][3]; out: [n * (S/patch)^2][Kp] bf16 (vpf_crop_patches_bf16) or fp32 (_f32).
- * norm_ab_host: 6 floats {a0,a1,a2,b0,b1,b2} (SPEC S3). Requires Kp % 8 == 0, Kp >= 3*patch^2. */
-int vpf_crop_patches_bf16(const uint8_t* frame, int H, int W, const float* particles, int64_t ld,
-                          int64_t n, float w0, float h0, int S, int patch, int Kp,
+ * frame: uint8[H][W][3]; rgba_ws: caller-owned workspace of (H+2)*(W+2) uint32 (the zero-bordered RGBA
+ * frame the taps read; rewritten by every call); out: [n * (S/patch)^2][Kp] bf16 (vpf_crop_patches_bf16) or
+ * fp32 (_f32). norm_ab_host: 6 floats {a0,a1,a2,b0,b1,b2} (SPEC S3). Requires Kp % 8 == 0, Kp >= 3*patch^2. */
+int vpf_crop_patches_bf16(const uint8_t* frame, int H, int W, uint32_t* rgba_ws, const float* particles,
+                          int64_t ld, int64_t n, float w0, float h0, int S, int patch, int Kp,
                           const float* norm_ab_host, uint16_t* out, void* stream);
-int vpf_crop_patches_f32(const uint8_t* frame, int H, int W, const float* particles, int64_t ld,
-                         int64_t n, float w0, float h0, int S, int patch, int Kp,
+int vpf_crop_patches_f32(const uint8_t* frame, int H, int W, uint32_t* rgba_ws, const float* particles,
+                         int64_t ld, int64_t n, float w0, float h0, int S, int patch, int Kp,
                          const float* norm_ab_host, float* out, void* stream);
 
 /* H3 (CLS row): tokens[p][0][:] = cls + pos[0] for p < n_part; tokens: [n_part][N][D]. */

@@ -64,11 +64,13 @@ def test_crop_bit_exact(S, patch, H, W):
     assert np.array_equal(np.array(ab[:3], np.float32), a) and np.array_equal(np.array(ab[3:], np.float32), b)
     fd, pd = torch.from_numpy(frame).to(DEV), torch.from_numpy(p).to(DEV)
     g = S // patch
+    from vitparticlefiltertracker_amd.ops import rgba_workspace
+    ws = rgba_workspace((H, W), DEV)
     out32 = torch.empty(n * g * g, kp, device=DEV, dtype=torch.float32)
-    vpf().crop_patches(fd, pd, list(box), S, patch, ab, out32)
+    vpf().crop_patches(fd, ws, pd, list(box), S, patch, ab, out32)
     assert np.array_equal(out32.cpu().numpy().view(np.uint32), ref.view(np.uint32))
     out16 = torch.empty(n * g * g, kp, device=DEV, dtype=torch.bfloat16)
-    vpf().crop_patches(fd, pd, list(box), S, patch, ab, out16)
+    vpf().crop_patches(fd, ws, pd, list(box), S, patch, ab, out16)
     assert np.array_equal(out16.cpu().view(torch.int16).numpy().view(np.uint16), bf16_bits(ref))
 
 

@@ -42,12 +42,20 @@ def predict_(particles: torch.Tensor, global_begin: int, seed: int, frame: int, 
          motion_std[1], motion_std[2], width, height, scale_range[0], scale_range[1], stream_ptr())
 
 
-@torch.library.custom_op("vpf::crop_patches", mutates_args={"out"}, device_types="cuda")
-def crop_patches(frame: torch.Tensor, particles: torch.Tensor, box_wh: List[float], img_size: int, patch: int,
-                 norm_ab: List[float], out: torch.Tensor) -> None:
-    """H2+H3 A operand, SPEC S3: out[n*g*g][Kp] (bf16 or f32)."""
-    _dev(frame, particles, out)
+def rgba_workspace(frame_hw, device) -> torch.Tensor:
+    """Workspace for crop_patches: int32[(H+2)*(W+2)] (the zero-bordered RGBA frame)."""
+    H, W = int(frame_hw[0]), int(frame_hw[1])
+    return torch.empty((H + 2) * (W + 2), device=device, dtype=torch.int32)
+
+
+@torch.library.custom_op("vpf::crop_patches", mutates_args={"rgba_ws", "out"}, device_types="cuda")
+def crop_patches(frame: torch.Tensor, rgba_ws: torch.Tensor, particles: torch.Tensor, box_wh: List[float],
+                 img_size: int, patch: int, norm_ab: List[float], out: torch.Tensor) -> None:
+    """H2+H3 A operand, SPEC S3: out[n*g*g][Kp] (bf16 or f32). rgba_ws: rgba_workspace(frame.shape[:2])."""
+    _dev(frame, rgba_ws, particles, out)
     _chk(frame.dtype == torch.uint8 and frame.dim() == 3 and frame.shape[2] == 3, "frame: u8[H][W][3]")
+    _chk(rgba_ws.dtype == torch.int32 and rgba_ws.is_contiguous()
+         and rgba_ws.numel() >= (frame.shape[0] + 2) * (frame.shape[1] + 2), "rgba_ws: int32[(H+2)*(W+2)]")
     _chk(particles.dtype == _F32 and particles.dim() == 2 and particles.shape[0] == 3, "particles: f32[3][n]")
     n = particles.shape[1]
     g = img_size // patch
@@ -58,8 +66,8 @@ def crop_patches(frame: torch.Tensor, particles: torch.Tensor, box_wh: List[floa
     abp = ab.ctypes.data_as(ctypes.c_void_p)
     name = "vpf_crop_patches_bf16" if out.dtype == _BF16 else "vpf_crop_patches_f32"
     _chk(out.dtype in (_BF16, _F32), "out dtype must be bf16 or f32")
-    call(name, ptr(frame), frame.shape[0], frame.shape[1], ptr(particles), n, n, box_wh[0], box_wh[1], img_size,
-         patch, kp, abp, ptr(out), stream_ptr())
+    call(name, ptr(frame), frame.shape[0], frame.shape[1], ptr(rgba_ws), ptr(particles), n, n, box_wh[0], box_wh[1],
+         img_size, patch, kp, abp, ptr(out), stream_ptr())
 
 
 @torch.library.custom_op("vpf::cls_rows_", mutates_args={"tokens"}, device_types="cuda")

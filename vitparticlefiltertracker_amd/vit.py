@@ -24,7 +24,7 @@ from typing import Dict, Optional
 import torch
 
 from . import _lib
-from . import ops  # noqa: F401  (registers torch.ops.vpf)
+from . import ops  # registers torch.ops.vpf; rgba_workspace
 from .config import ViTArch
 
 vpf = torch.ops.vpf
@@ -161,7 +161,11 @@ class ViTEngine:
         n = particles.shape[1]
         patches = self.patches[: n * A.n_patches]
         T = self.timer
-        _run(T, "crop_patches", vpf.crop_patches, frame, particles, [float(box_wh[0]), float(box_wh[1])],
+        hw = (int(frame.shape[0]), int(frame.shape[1]))
+        if getattr(self, "_rgba_hw", None) != hw:          # workspace sized for this frame shape
+            self.rgba = ops.rgba_workspace(hw, frame.device)
+            self._rgba_hw = hw
+        _run(T, "crop_patches", vpf.crop_patches, frame, self.rgba, particles, [float(box_wh[0]), float(box_wh[1])],
              A.img_size, A.patch, self.norm_ab, patches)
         h = self.h[:n]
         _run(T, "gemm_patch", vpf.gemm, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches, None, None,
