@@ -11,7 +11,9 @@ resample (+ RCCL all-gathers when N > 1). Frames (synthetic u8 224x224, moving t
 resident in HBM before the timed region. Rank 0 prints ONE JSON line. Extra fields:
   roofline      the dominant kernel (the FC1 GEMM by default: the largest FLOP share) timed by HIP events on
                 its own stream in an eager pass after the timed region: achieved TFLOP/s vs the 2.5 PF dense
-                bf16 MFMA peak (MI355X_MICROARCH.md). traffic = null (PMC pass: profiles/).
+                bf16 MFMA peak (MI355X_MICROARCH.md). traffic = HBM bytes per launch of that kernel from the
+                committed PMC summary profiles/r1_pmc_traffic.json (tools/gpu_session.sh pmc), when taken on
+                this workload; else null.
   frame_mfma_frac  whole-frame algorithmic FLOPs (35.126 GFLOP/crop) x fps / peak.
   kernels       per-kernel-type HIP-event averages from the same eager pass.
   cpu_baseline  the CPU oracle (torch fp32 ViT + C particle-filter ops, "port": the reference has no
@@ -31,6 +33,24 @@ sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec @ 4096 particles, ViT-B/16 224px; 1/2/4/8 MI355X scaling"
 PEAK_BF16_TFLOPS = 2500.0
+
+
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+
+
+def pmc_traffic(arch_name: str, n_local: int, kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_traffic.py over two
+    rocprofv3 passes of this bench: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when it was taken on the
+    same workload; otherwise (None, reason)."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+        if d.get("arch") != arch_name or int(d.get("particles_per_gpu", -1)) != n_local:
+            return None, "no PMC summary for this workload"
+        k = d["kernels"][kernel]
+        return int(k["traffic_bytes"]), os.path.relpath(PMC_TRAFFIC, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, "no PMC summary"
 
 
 def parse():
@@ -163,6 +183,7 @@ def main() -> int:
             v["tflops"] = flops[name] / (v["avg_ms"] * 1e-3) / 1e12
     dom = max((n for n in flops if n.startswith("gemm") and n in ks), key=lambda n: ks[n]["total_ms"])
     ach = ks[dom]["tflops"]
+    traffic, traffic_src = pmc_traffic(args.arch, n_loc, dom)
     gflop_frame = arch.gflop_per_crop() * args.particles
     line = {
         "metric": METRIC,
@@ -182,7 +203,8 @@ def main() -> int:
                    "particles": args.particles, "particles_per_gpu": n_loc, "arch": args.arch,
                    "hip_graph": not args.no_graph, "parallelism": f"particle-shard x{world}"},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "avg_launch_ms": round(ks[dom]["avg_ms"], 4),
                      "flop_per_launch": flops[dom]},
         "frame_mfma_frac": round(gflop_frame * 1e9 * fps / (PEAK_BF16_TFLOPS * 1e12 * world), 4),

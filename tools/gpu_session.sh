@@ -30,6 +30,14 @@ for step in "$@"; do
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/prof.log 2>&1
       ok_or_stop $? prof; tail -3 $OUT/prof.log ;;
+    pmc)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc_fetch -o p --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernel-frames 1 --cpu-seconds 0 --no-graph > $OUT/pmc_fetch.log 2>&1
+      ok_or_stop $? pmc_fetch
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc_write -o p --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernel-frames 1 --cpu-seconds 0 --no-graph > $OUT/pmc_write.log 2>&1
+      ok_or_stop $? pmc_write
+      python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write > $OUT/pmc_traffic.json 2> $OUT/pmc_traffic.err
+      ok_or_stop $? pmc_traffic; cat $OUT/pmc_traffic.json | head -40 ;;
     lab)
       timeout -k 10 600 tools/gemm_lab/gemm_lab 5 "$LAB_SHAPES" "$LAB_VARS" 1 > $OUT/lab.log 2>&1
       ok_or_stop $? lab; grep -v "inf TFLOP" $OUT/lab.log | tail -40 ;;

@@ -316,6 +316,100 @@ void k_attn_bf16_pers(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, 
     if (has_strip) store_o(prev, wid, o0, o1, l);
 }
 
+
+// CLS-only attention (q_rows == 1: the last encoder block, whose other query rows feed nothing): one wave
+// per (particle, head), 4 per workgroup, no LDS, so occupancy is set by VGPRs and many heads stream K / V
+// at once (the path is pure HBM streaming: 2 x N x 128 B per head for one query).
+//   scores: lane j owns keys j, j+64, ...; K rows read whole (128 B) from global; fp32 dot with the CLS
+//           query (broadcast loads), wave max / sum -> fp32 softmax in the exp2 domain;
+//   PV:     lane (g, d8) = (lane >> 3, lane & 7) accumulates dims 8*d8..8*d8+7 over keys j = g (mod 8),
+//           probabilities fetched with ds_bpermute, then a 3-step shuffle reduction over g.
+constexpr int CLS_MAXT = 10;   // keys per lane in the score phase: N <= 640
+__global__ __launch_bounds__(256) void k_attn_cls_bf16(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                       int N, int H, int BH, float scale_log2) {
+    const int lane = threadIdx.x & 63;
+    const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (bh >= BH) return;
+    const int b = bh / H, h = bh - (bh / H) * H;
+    const int D = H * HD;
+    const bf16_t* base = qkv + (int64_t)b * N * 3 * D + h * HD;
+    float q[HD];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const uint4 u = *reinterpret_cast<const uint4*>(base + c * 8);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            q[c * 8 + 2 * e] = bf2f((bf16_t)(w[e] & 0xffff));
+            q[c * 8 + 2 * e + 1] = bf2f((bf16_t)(w[e] >> 16));
+        }
+    }
+    float sc[CLS_MAXT];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < CLS_MAXT; ++t) {
+        const int j = lane + 64 * t;
+        float sv = -INFINITY;
+        if (j < N) {
+            const bf16_t* kr = base + (int64_t)j * 3 * D + D;
+            float acc = 0.f;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint4 u = *reinterpret_cast<const uint4*>(kr + c * 8);
+                const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    acc = fmaf(q[c * 8 + 2 * e], bf2f((bf16_t)(w[e] & 0xffff)), acc);
+                    acc = fmaf(q[c * 8 + 2 * e + 1], bf2f((bf16_t)(w[e] >> 16)), acc);
+                }
+            }
+            sv = acc * scale_log2;
+        }
+        sc[t] = sv;
+        mx = fmaxf(mx, sv);
+    }
+    mx = wave_max(mx);
+    float l = 0.f;
+#pragma unroll
+    for (int t = 0; t < CLS_MAXT; ++t) {
+        sc[t] = (lane + 64 * t < N) ? __builtin_amdgcn_exp2f(sc[t] - mx) : 0.f;
+        l += sc[t];
+    }
+    l = wave_sum(l);
+    const int g = lane >> 3, d8 = lane & 7;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < CLS_MAXT; ++t) {
+        if (64 * t >= N) break;
+#pragma unroll
+        for (int ii = 0; ii < 8; ++ii) {
+            const int j = 64 * t + 8 * ii + g;            // keys of this (t, ii) block: 8 consecutive
+            const float pj = __shfl(sc[t], 8 * ii + g, 64);
+            if (j < N) {
+                const uint4 u = *reinterpret_cast<const uint4*>(base + (int64_t)j * 3 * D + 2 * D + d8 * 8);
+                const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    o[2 * e] = fmaf(pj, bf2f((bf16_t)(w[e] & 0xffff)), o[2 * e]);
+                    o[2 * e + 1] = fmaf(pj, bf2f((bf16_t)(w[e] >> 16)), o[2 * e + 1]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        o[e] += __shfl_xor(o[e], 8, 64);
+        o[e] += __shfl_xor(o[e], 16, 64);
+        o[e] += __shfl_xor(o[e], 32, 64);
+    }
+    if (g == 0) {
+        const float inv = 1.0f / l;
+        bf16_t* orow = out + (int64_t)b * N * D + h * HD + d8 * 8;
+        *reinterpret_cast<uint4*>(orow) = make_uint4(pack_bf2(o[0] * inv, o[1] * inv), pack_bf2(o[2] * inv, o[3] * inv),
+                                                     pack_bf2(o[4] * inv, o[5] * inv), pack_bf2(o[6] * inv, o[7] * inv));
+    }
+}
+
 // ---------------- fp32 parity path ----------------
 // One thread per query; K / V of the (particle, head) stream through LDS in chunks of KC keys, so any N
 // works (ViT-L/14 @ 336: N = 577). Exact two-pass softmax in key order: pass 1 the row max over all keys,
@@ -402,6 +496,11 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     const float scale_log2 = scale * 1.44269504088896341f;
     const int strips = (q_rows + 31) / 32;
     const int64_t BH = B * H;
+    if (q_rows == 1) {
+        hipLaunchKernelGGL(k_attn_cls_bf16, dim3((unsigned)((BH + 3) / 4)), dim3(256), 0, (hipStream_t)stream, qkv, out,
+                           N, H, (int)BH, scale_log2);
+        VPF_RETURN_LAUNCH();
+    }
     const char* mode = getenv("VPF_ATTN_MODE");   // "1": persistent double-buffered kernel (design aid)
     if (mode && mode[0] == '1' && 2 * lds <= 150 * 1024 && BH >= 4 * cu_count()) {
         static bool pattr = false;   // benign race: idempotent attribute set

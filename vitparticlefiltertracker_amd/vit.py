@@ -174,8 +174,9 @@ class ViTEngine:
 
     def encoder(self, n: int) -> None:
         """L pre-norm blocks on h[:n]. The last block only needs the CLS rows after its attention (the
-        final LN reads nothing else), so its attention computes q_rows = 1 and its proj / MLP run on the
-        n strided CLS rows (outputs identical to the full block's CLS rows)."""
+        final LN reads nothing else): its QKV GEMM computes K, V for every row but Q for the CLS rows only,
+        its attention computes the CLS query only (q_rows = 1), and its proj / MLP run on the n strided CLS
+        rows."""
         A = self.arch
         D, N, F = A.dim, A.tokens, A.mlp
         T = self.timer
@@ -193,16 +194,31 @@ class ViTEngine:
         fold = self.fold_ln
         if fold:
             _run(T, "row_stats", vpf.row_stats, h2, A.ln_eps, st)
+        q2 = qkv.view(n * N, 3 * D)
+        kv2 = q2[:, D:]                                 # K | V columns of every row
+        qc = qkv.view(n, N * 3 * D)[:, :D]             # Q columns of the CLS rows
         for l, L in enumerate(self.layers):
             last = l == len(self.layers) - 1
+            # the last block's attention reads only the CLS query: K, V for every row, Q for the CLS rows
             if fold:
-                _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, st, L["cqkv"], LNE,
-                     qkv.view(n * N, 3 * D))
+                if not last:
+                    _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, st, L["cqkv"], LNE, q2)
+                else:
+                    _run(T, "gemm_kv", vpf.gemm, h2, L["wqkv"][D:], L["bqkv"][D:], None, None, 0, st, L["cqkv"][D:],
+                         LNE, kv2)
+                    _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # st already consumed above
+                    _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc,
+                         L["cqkv"][:D], LNE, qc)
             else:
                 _run(T, "layernorm", vpf.layernorm, h2, L["n1g"], L["n1b"], A.ln_eps, x2)
-                _run(T, "gemm_qkv", vpf.gemm, x2, L["wqkv"], L["bqkv"], None, None, 0, None, None, BIAS,
-                     qkv.view(n * N, 3 * D))
-            _run(T, "attention", vpf.attention, qkv, A.heads, 1 if last else N, self.x[:n])
+                if not last:
+                    _run(T, "gemm_qkv", vpf.gemm, x2, L["wqkv"], L["bqkv"], None, None, 0, None, None, BIAS, q2)
+                else:
+                    _run(T, "gemm_kv", vpf.gemm, x2, L["wqkv"][D:], L["bqkv"][D:], None, None, 0, None, None, BIAS,
+                         kv2)
+                    _run(T, "gemm_q_cls", vpf.gemm, xc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, None, None,
+                         BIAS, qc)
+            _run(T, "attention_cls" if last else "attention", vpf.attention, qkv, A.heads, 1 if last else N, self.x[:n])
             hh, xx, hd_, ss = (hc, xc, hidc, stc) if last else (h2, x2, hid, st)
             tag = "_cls" if last else ""
             _run(T, "gemm_proj" + tag, vpf.gemm, xx, L["wproj"], L["bproj"], hh, None, 0, None, None, RES, hh)
