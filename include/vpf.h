@@ -73,6 +73,11 @@ int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, const float
                   const uint16_t* residual, const float* pos, int patch_rows, const float* row_stats,
                   const float* colsum, uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                   int epilogue, void* stream);
+/* Tuning knob for vpf_gemm_bf16 (process-wide; call it only between launches). kernel: 1 = one 256x256
+ * tile per 512-thread workgroup, 2 = two 256x128-tile workgroups per CU (K % 32 == 0), 3..8 = measurement
+ * variants (tools/gemm_ab.py). group: A-panel group size of the tile order (0 = row-major; < 0 = keep).
+ * Initial values come from VPF_GEMM_KERNEL / VPF_GEMM_GROUP. Returns VPF_ERR_ARG for an unknown kernel. */
+int vpf_gemm_tune(int kernel, int group);
 /* fp32 parity mode: same contract with fp32 tensors (exact-f32 MFMA, v_mfma_f32_32x32x2_f32).
  * Requires K % 32 == 0, lda % 4 == 0, ldc % 4 == 0. */
 int vpf_gemm_f32(const float* A, int64_t lda, const float* W, const float* bias, const float* residual,

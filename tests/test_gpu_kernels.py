@@ -149,6 +149,22 @@ def test_gemm_f32(M, N, K, epi):
     torch.testing.assert_close(out.double(), ref, rtol=2e-5, atol=2e-5)
 
 
+def test_gemm_bf16_gelu_accuracy():
+    """The bf16 GEMM's GELU epilogue (sigmoid form, gelu_sig2) against the exact-erf GELU: A W^T is made exact
+    (W = I, one nonzero term per output) so the only error left is the GELU's and the bf16 output rounding.
+    Bar: |gelu_sig2(x) - gelu(x)| <= 2.8e-4 (the minimax bound) plus half a bf16 ulp of the result."""
+    M, K = 4096, 128
+    x = torch.linspace(-10, 10, M * K, device=DEV).reshape(M, K).to(torch.bfloat16)
+    W = torch.eye(K, device=DEV, dtype=torch.bfloat16)
+    bias = torch.zeros(K, device=DEV)
+    out = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    vpf().gemm(x, W, bias, None, None, 0, None, None, 1, out)
+    ref = Fn.gelu(x.double())
+    half_ulp = ref.abs().clamp_min(2.0 ** -126) * 2.0 ** -8   # bf16: 8 significant bits
+    err = (out.double() - ref).abs()
+    assert torch.all(err <= 2.8e-4 + half_ulp), float((err - half_ulp).max())
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("gelu", [False, True])
 def test_gemm_layernorm_fold(dtype, gelu):
