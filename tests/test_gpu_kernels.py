@@ -281,11 +281,12 @@ def test_attention_q_rows(dtype, B, N, H):
     assert torch.all(part2[:, 2:] == 5.0)
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("mode", ["0", "2"])
 @pytest.mark.parametrize("B,N,H", [(100, 197, 12), (90, 256, 12), (96, 280, 12)])
 def test_attention_bf16_large(B, N, H, mode, monkeypatch):
-    """B*H >= 4 x CUs. mode "1" selects the persistent double-buffered kernel (VPF_ATTN_MODE); N = 280 has 9
-    query strips, so a wave also takes a second strip. Both kernels must agree bit for bit."""
+    """B*H >= 4 x CUs. mode "0" forces the whole-image kernel (VPF_ATTN_MODE), "2" the default (key-pipelined
+    for N <= 256); N = 280 has 9 query strips, so a wave also takes a second strip. Both kernels must agree bit
+    for bit."""
     torch.manual_seed(N + H)
     D = 64 * H
     qkv = (torch.randn(B, N, 3 * D, device=DEV) * 1.5).to(torch.bfloat16)
@@ -306,7 +307,7 @@ def test_attention_bf16_large(B, N, H, mode, monkeypatch):
     assert torch.all(part[:, 1:] == 5.0)
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("mode", ["0", "2"])
 def test_attention_bf16_rescale_branch(mode, monkeypatch):
     """The lazy online-softmax rescale only runs when a query's max grows by > 2^8 (exp2 domain) within a
     key tile: force it (a key row aligned with a query, late in the sequence) and also plant spikes below the

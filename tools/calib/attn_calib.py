@@ -1,4 +1,4 @@
-"""Design aid: libvpf attention kernels (VPF_ATTN_MODE 0 = per-(particle, head) workgroups, 1 = persistent
+"""Design aid: libvpf attention kernels (VPF_ATTN_MODE 0 = whole-image per-(particle, head) workgroups, 2 = key-pipelined (default for N <= 256)
 double-buffered) on the ViT-B/16 shape at 4096 particles, interleaved rounds in one process."""
 import os, sys
 import torch
@@ -6,6 +6,7 @@ sys.path.insert(0, ".")
 from vitparticlefiltertracker_amd import ops
 
 B, N, H = 4096, 197, 12
+MODES = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1"]
 D = 64 * H
 torch.manual_seed(0)
 qkv = (torch.randn(B, N, 3 * D, device="cuda") * 1.5).to(torch.bfloat16)
@@ -14,12 +15,12 @@ bytes_ = qkv.numel() * 2 + out.numel() * 2
 fl = 4.0 * B * H * N * N * 64
 res = {}
 for _ in range(2):
-    for m in ("0", "1"):
+    for m in MODES:
         os.environ["VPF_ATTN_MODE"] = m
         ops.attention(qkv, H, N, out)
 torch.cuda.synchronize()
 for _ in range(7):
-    for m in ("0", "1"):
+    for m in MODES:
         os.environ["VPF_ATTN_MODE"] = m
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

@@ -21,6 +21,9 @@ SHAPES = {  # name: (N, K, epilogue)
     "proj": (768, 768, E.VPF_EPI_BIAS_RESIDUAL),
     "fc1": (3072, 768, E.VPF_EPI_LN_GELU),
     "fc2": (768, 3072, E.VPF_EPI_BIAS_RESIDUAL),
+    "proj_bias": (768, 768, E.VPF_EPI_BIAS),
+    "fc1_bias": (3072, 768, E.VPF_EPI_BIAS),
+    "fc2_bias": (768, 3072, E.VPF_EPI_BIAS),
 }
 
 

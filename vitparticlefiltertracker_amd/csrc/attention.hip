@@ -50,7 +50,17 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // update of (m, l, O), O^T += V^T P^T with V^T fragments from transposed LDS reads. MASK: this step contains
 // padded keys (only the last step). The O / l rescale is skipped when no query's running max moved in this
 // step (wave-uniform test), which is the common case after the first key tiles.
-template <int T, bool MASK>
+// ds_read_b64_tr_b16 as inline asm: hipcc treats the builtin as a possible reader of in-flight LDS-DMA
+// bytes and drains vmcnt(0) before it, which would serialise the key-pipelined kernel on its last chunk.
+// The caller waits lgkmcnt itself (tr_wait) before the MFMA that consumes the result.
+__device__ __forceinline__ bf16x4 ds_read_tr_asm(const char* lds_base, int byte_off) {
+    bf16x4 r;
+    const uint32_t a = (uint32_t)(size_t)lds_base + (uint32_t)byte_off;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+
+template <int T, bool MASK, bool ASM_TR = false>
 __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb, int N, int lane, const bf16x8 qf[4],
                                           float scale_log2, float& m, float& l, f32x16& o0, f32x16& o1) {
     const int l32 = lane & 31, hh = lane >> 5;
@@ -110,6 +120,34 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
     }
     const int grp = lane >> 4, gi = lane & 15;
     const int rq = gi >> 2, cp = gi & 3;
+    if constexpr (ASM_TR) {
+        static_assert(T == 1, "asm transposed-read path handles one 32-key tile");
+        bf16x4 vr[2][2][2];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            const int rbase = kb + st * 16 + 4 * (grp >> 1) + rq;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
+                const int c16 = col >> 3, inner = (col & 7) * 2;
+                vr[st][dt][0] = ds_read_tr_asm(Vs, v_off(rbase, c16) + inner);
+                vr[st][dt][1] = ds_read_tr_asm(Vs, v_off(rbase + 8, c16) + inner);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1]),
+                     "+v"(vr[1][0][0]), "+v"(vr[1][0][1]), "+v"(vr[1][1][0]), "+v"(vr[1][1][1])::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const bf16x4 lo = vr[st][dt][0], hi = vr[st][dt][1];
+                const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][st], o0, 0, 0, 0);
+                else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][st], o1, 0, 0, 0);
+            }
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -204,55 +242,87 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 
-// Persistent variant (N <= 312, i.e. two K/V images fit in LDS): one 512-thread workgroup per CU walks
-// (particle, head) pairs bh = blockIdx.x, + gridDim.x, ... K/V of the next pair are DMA'd
-// (global_load_lds, 16 B per lane, swizzle on the source address) into the other half of a double-buffered
-// LDS image while the current pair computes, and the next pair's Q fragments are prefetched into registers,
-// so HBM streaming overlaps the MFMA/softmax work instead of alternating with it. A pair's output is stored
-// after the barrier that ends it, so the per-pair vmcnt(0) (which retires the next pair's DMA) never waits
-// on fresh stores. Rows >= N of the images are filled from row N-1 (finite values; their keys are masked
-// and their probabilities are exactly 0).
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-void k_attn_bf16_pers(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, int BH,
-                      float scale_log2, int q_rows) {
+// s_waitcnt vmcnt(n) for a runtime n (the immediate must be a constant): n >= the outstanding count is a no-op
+__device__ __forceinline__ void wait_vmcnt(int n) {
+    switch (n) {
+#define VPF_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+        VPF_VMW(1) VPF_VMW(2) VPF_VMW(3) VPF_VMW(4) VPF_VMW(5) VPF_VMW(6) VPF_VMW(7) VPF_VMW(8) VPF_VMW(9)
+        VPF_VMW(10) VPF_VMW(11) VPF_VMW(12) VPF_VMW(13) VPF_VMW(14) VPF_VMW(15) VPF_VMW(16) VPF_VMW(17)
+        VPF_VMW(18) VPF_VMW(19) VPF_VMW(20) VPF_VMW(21) VPF_VMW(22) VPF_VMW(23)
+#undef VPF_VMW
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+// Key-pipelined variant: one 512-thread workgroup per (particle, head) as above, but the K/V images land in
+// 32-key chunks and compute follows them: every wave issues its Q loads, then exactly one DMA piece per
+// chunk (waves 0-3: the chunk's four 8-row K pieces, waves 4-7: its four V pieces), in chunk order. Key tile
+// c is computed after a counted vmcnt (this wave's pieces of chunks <= c landed; later chunks stay in
+// flight) and one s_barrier (everyone's did), so the QK^T / softmax / PV of the first tiles overlap the
+// HBM fetch of the later ones instead of waiting for the whole 57 KiB image. Waves without a query strip
+// (8 waves, 7 strips at N = 197) only move data and keep the barrier count. N <= 256 (one strip per wave).
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_pipe(
+    const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int NP = (N + 31) & ~31;
-    const int IMG = NP * ROWB;            // one K or V image
+    const int NT = NP >> 5;              // 32-key chunks
+    char* Ks = smem;
+    char* Vs = smem + NP * ROWB;
+    const int bh = blockIdx.x;
+    const int b = bh / H, h = bh - (bh / H) * H;
+    const int D = H * HD;
+    const int64_t row0 = (int64_t)b * N;
+    const bf16_t* qbase = qkv + row0 * 3 * D + h * HD;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int D = H * HD;
     const int l32 = lane & 31, hh = lane >> 5;
     const int nstrips = (q_rows + 31) >> 5;
-    const int ninstr = NP >> 3;           // 8 rows (1 KiB) per DMA wave-instruction, per image
-    const int sub = lane >> 3, slot = lane & 7;
 
-    auto issue_kv = [&](int bh, int buf) {
-        const int b = bh / H, h = bh - (bh / H) * H;
-        const bf16_t* base = qkv + (int64_t)b * N * 3 * D + h * HD;
-        char* kimg = smem + buf * 2 * IMG;
-        char* vimg = kimg + IMG;
-        for (int j = wid; j < 2 * ninstr; j += 8) {
-            const bool isv = j >= ninstr;
-            const int g = isv ? j - ninstr : j;
-            const int r = 8 * g + sub;
-            const int c = isv ? (slot ^ (((r >> 1) & 1) << 2)) : (slot ^ ((r >> 1) & 7));
-            const bf16_t* src = base + (int64_t)min(r, N - 1) * 3 * D + (isv ? 2 * D : D) + c * 8;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)((isv ? vimg : kimg) + g * 1024), 16, 0, 0);
-        }
-    };
-    auto load_q = [&](int bh, int strip, bf16x8 (&qf)[4]) {
-        const int b = bh / H, h = bh - (bh / H) * H;
-        const int q = strip * 32 + l32;
-        const bf16_t* qb = qkv + ((int64_t)b * N + min(q, N - 1)) * 3 * D + h * HD + hh * 8;
+    const int q = wid * 32 + l32;
+    // Q fragments by inline-asm loads: hipcc does not count them, so it cannot merge them into a vmcnt(0) at
+    // the first MFMA (which would also drain every K/V chunk). They are older than all DMA pieces, so the
+    // first chunk's counted wait retires them; the empty asm after it pins every use below that wait.
+    bf16x8 qf[4];
+    {
+        const bf16_t* qp = qbase + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qb + ks * 16);
-    };
-    auto store_o = [&](int bh, int strip, const f32x16& o0, const f32x16& o1, float l) {
-        const int q = strip * 32 + l32;
-        if (q >= q_rows) return;
-        const int b = bh / H, h = bh - (bh / H) * H;
-        const float inv = 1.0f / l;
-        bf16_t* orow = out + ((int64_t)b * N + q) * D + h * HD;
+        for (int ks = 0; ks < 4; ++ks) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + ks * 16));
+    }
+    {
+        const bool isv = wid >= 4;
+        const int sub = lane >> 3, slot = lane & 7;
+        const bf16_t* src0 = qbase + (isv ? 2 * D : D);
+        char* img = isv ? Vs : Ks;
+        for (int c = 0; c < NT; ++c) {
+            const int g = c * 4 + (wid & 3);                 // 8-row piece index inside the image
+            const int r = 8 * g + sub;
+            const int ch = isv ? (slot ^ (((r >> 1) & 1) << 2)) : (slot ^ ((r >> 1) & 7));
+            __builtin_amdgcn_global_load_lds((gptr_t)(src0 + (int64_t)min(r, N - 1) * 3 * D + ch * 8),
+                                             (lptr_t)(img + g * 1024), 16, 0, 0);
+        }
+    }
+    const bool active = wid < nstrips;
+    f32x16 o0 = {}, o1 = {};
+    float m = -INFINITY, l = 0.f;
+    const int nfull = N >> 5;             // chunks without padded keys
+    int c = 0;
+    for (; c < nfull; ++c) {
+        wait_vmcnt(NT - 1 - c);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        if (active) attn_step<1, false, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+    }
+    if (c < NT) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        if (active) attn_step<1, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+    }
+    if (!active) return;
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+    if (q < q_rows) {
+        bf16_t* orow = out + (row0 + q) * D + h * HD;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
             const int d = 8 * g4 + 4 * hh;
@@ -261,59 +331,7 @@ void k_attn_bf16_pers(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, 
             *reinterpret_cast<uint2*>(orow + 32 + d) =
                 make_uint2(pack_bf2(o1[4 * g4] * inv, o1[4 * g4 + 1] * inv), pack_bf2(o1[4 * g4 + 2] * inv, o1[4 * g4 + 3] * inv));
         }
-    };
-
-    int bh = blockIdx.x;
-    if (bh >= BH) return;
-    const bool has_strip = wid < nstrips;
-    bf16x8 qn[4];
-    issue_kv(bh, 0);
-    if (has_strip) load_q(bh, wid, qn);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    f32x16 o0 = {}, o1 = {};
-    float l = 1.f;
-    int prev = -1;
-    for (int it = 0; bh < BH; ++it, bh += gridDim.x) {
-        const int buf = it & 1;
-        const int nbh = bh + gridDim.x;
-        if (prev >= 0 && has_strip) store_o(prev, wid, o0, o1, l);     // previous pair's strip
-        if (nbh < BH) issue_kv(nbh, buf ^ 1);
-        bf16x8 qf[4];
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) qf[ks] = qn[ks];
-        if (nbh < BH && has_strip) load_q(nbh, wid, qn);
-        const char* Ks = smem + buf * 2 * IMG;
-        const char* Vs = Ks + IMG;
-        const int nfull = N & ~31;
-        // extra strips (N > 256) first, stored at once; the wave's own strip last, so its accumulators are the
-        // ones kept for the deferred store after the barrier
-        int last = wid;
-        while (last + 8 < nstrips) last += 8;
-        for (int strip = last; strip >= wid && strip < nstrips; strip -= 8) {
-            bf16x8 qs[4];
-            if (strip != wid) {
-                load_q(bh, strip, qs);
-            } else {
-#pragma unroll
-                for (int ks = 0; ks < 4; ++ks) qs[ks] = qf[ks];
-            }
-            o0 = f32x16{};
-            o1 = f32x16{};
-            float m = -INFINITY;
-            l = 0.f;
-            int kb = 0;
-            for (; kb < nfull; kb += 32) attn_step<1, false>(Ks, Vs, kb, N, lane, qs, scale_log2, m, l, o0, o1);
-            if (kb < NP) attn_step<1, true>(Ks, Vs, kb, N, lane, qs, scale_log2, m, l, o0, o1);
-            l += __shfl_xor(l, 32, 64);
-            if (strip != wid) store_o(bh, strip, o0, o1, l);
-        }
-        prev = bh;
-        // retires the next pair's K/V DMA and Q prefetch (issued one pair ago) and the stores of the pair before
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
     }
-    if (has_strip) store_o(prev, wid, o0, o1, l);
 }
 
 
@@ -501,17 +519,18 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
                            N, H, (int)BH, scale_log2);
         VPF_RETURN_LAUNCH();
     }
-    const char* mode = getenv("VPF_ATTN_MODE");   // "1": persistent double-buffered kernel (design aid)
-    if (mode && mode[0] == '1' && 2 * lds <= 150 * 1024 && BH >= 4 * cu_count()) {
-        static bool pattr = false;   // benign race: idempotent attribute set
-        if (!pattr) {
-            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pers, hipFuncAttributeMaxDynamicSharedMemorySize,
+    // N <= 256: the key-pipelined kernel (8 waves, one strip each). VPF_ATTN_MODE=0 selects the
+    // whole-image kernel instead (A/B timing); N > 256 always takes it (waves loop over strips).
+    const char* mode = getenv("VPF_ATTN_MODE");
+    if (N <= 256 && !(mode && mode[0] == '0')) {
+        static bool pipe_attr = false;   // benign race: idempotent attribute set
+        if (!pipe_attr) {
+            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024);
-            pattr = true;
+            pipe_attr = true;
         }
-        const int grid = cu_count();
-        hipLaunchKernelGGL(k_attn_bf16_pers, dim3((unsigned)grid), dim3(512), 2 * lds, (hipStream_t)stream, qkv, out,
-                           N, H, (int)BH, scale_log2, q_rows);
+        hipLaunchKernelGGL(k_attn_bf16_pipe, dim3((unsigned)(B * H)), dim3(512), lds, (hipStream_t)stream, qkv, out,
+                           N, H, scale_log2, q_rows);
         VPF_RETURN_LAUNCH();
     }
     const int threads = 64 * (strips < 8 ? strips : 8);
