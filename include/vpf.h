@@ -56,9 +56,11 @@ int vpf_crop_patches_f32(const uint8_t* frame, int H, int W, uint32_t* rgba_ws, 
                          int64_t ld, int64_t n, float w0, float h0, int S, int patch, int Kp,
                          const float* norm_ab_host, float* out, void* stream);
 
-/* H3 (CLS row): tokens[p][0][:] = cls + pos[0] for p < n_part; tokens: [n_part][N][D]. */
+/* H3 (CLS row): tokens[p][0][:] = cls + pos[0] for p < n_part; tokens: [n_part][N][D].
+ * stats_out (bf16 only, may be NULL): the CLS rows' entries of the GEMM stats planes (see vpf_gemm_bf16):
+ * fp32[parts][n_part*N][2], plane 0 row p*N = {sum, sumsq} of the stored bf16 row, planes 1.. = 0. */
 int vpf_cls_rows_bf16(uint16_t* tokens, int64_t n_part, int N, int D, const float* cls,
-                      const float* pos, void* stream);
+                      const float* pos, float* stats_out, int parts, void* stream);
 int vpf_cls_rows_f32(float* tokens, int64_t n_part, int N, int D, const float* cls, const float* pos,
                      void* stream);
 
@@ -66,13 +68,18 @@ int vpf_cls_rows_f32(float* tokens, int64_t n_part, int N, int D, const float* c
  * Row m of A at A + m*lda; row m of C (and of the residual, which has C's layout) at C + m*ldc.
  * bias: fp32[N]; residual: bf16 (EPI_BIAS_RESIDUAL, may alias C); pos: fp32[g2+1][N] (EPI_PATCH, with
  * g2 = patch_rows, M % g2 == 0); EPI_LN / EPI_LN_GELU (LayerNorm folded into the GEMM, A = the raw
- * residual stream): row_stats fp32[M][2] = {mean, rstd} of A's rows (vpf_row_stats_*), W = W * diag(gamma),
- * colsum fp32[N] = sum_k W[n][k] (of the bf16 W), bias = b + W_orig beta. Unused pointers may be NULL.
- * Requires K % 64 == 0, N % 8 == 0, lda % 8 == 0, ldc % 8 == 0. */
+ * residual stream): W = W * diag(gamma), colsum fp32[N] = sum_k W[n][k] (of the bf16 W), bias = b + W_orig beta,
+ * and row_stats either (stats_parts == 0) fp32[M][2] = {mean, rstd} of A's rows (vpf_row_stats_*), or
+ * (stats_parts = P in 1..4) fp32[P][M][2] planes of {sum, sumsq} over disjoint column blocks of A's rows (the
+ * stats_out of the GEMM that produced A), combined with eps = ln_eps: rstd = 1/sqrt(sumsq/K - mean^2 + eps).
+ * stats_out (EPI_BIAS_RESIDUAL / EPI_PATCH only, may be NULL): fp32[ceil(N/256)][R][2] planes, plane t =
+ * {sum, sumsq} of the stored bf16 values of each output row over columns [256t, 256t+256); R = M, or
+ * (M/g2)*(g2+1) token rows for EPI_PATCH (plane rows of the CLS tokens are left to vpf_cls_rows_bf16).
+ * Unused pointers may be NULL. Requires K % 64 == 0, N % 8 == 0, lda % 8 == 0, ldc % 8 == 0. */
 int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, const float* bias,
                   const uint16_t* residual, const float* pos, int patch_rows, const float* row_stats,
                   const float* colsum, uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                  int epilogue, void* stream);
+                  int epilogue, int stats_parts, float ln_eps, float* stats_out, void* stream);
 /* Tuning knob for vpf_gemm_bf16 (process-wide; call it only between launches). kernel: 1 = one 256x256
  * tile per 512-thread workgroup, 2 = two 256x128-tile workgroups per CU (K % 32 == 0), 3..8 = measurement
  * variants (tools/gemm_ab.py). group: A-panel group size of the tile order (0 = row-major; < 0 = keep).

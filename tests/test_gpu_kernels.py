@@ -192,6 +192,67 @@ def test_gemm_layernorm_fold(dtype, gelu):
     torch.testing.assert_close(out.double(), ref, **tol)
 
 
+def _planes_ref(y: torch.Tensor, P: int) -> torch.Tensor:
+    """fp64 {sum, sumsq} per 256-column block of the rows of y (the vpf_gemm_bf16 stats_out layout)."""
+    yd = y.double()
+    out = []
+    for t in range(P):
+        b = yd[:, 256 * t: 256 * (t + 1)]
+        out.append(torch.stack([b.sum(1), (b * b).sum(1)], 1))
+    return torch.stack(out)
+
+
+@pytest.mark.parametrize("M,D", [(777, 768), (300, 192), (513, 1024)])
+def test_gemm_stats_planes(M, D):
+    """Residual-stream statistics planes (bf16 LN fold without a row_stats pass): the EPI_BIAS_RESIDUAL producer
+    writes {sum, sumsq} of its stored bf16 rows per 256-column block; an EPI_LN consumer reading those planes
+    (stats_parts = P, ln_eps) equals LayerNorm -> GEMM on the same rows."""
+    torch.manual_seed(M + D)
+    P = (D + 255) // 256
+    x = (torch.randn(M, D, device=DEV) * 0.7).to(torch.bfloat16)
+    W = (torch.randn(D, D, device=DEV) / D ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(D, device=DEV) * 0.1
+    h = (torch.randn(M, D, device=DEV) + 0.3).to(torch.bfloat16)
+    planes = torch.full((P, M, 2), float("nan"), device=DEV)
+    vpf().gemm_stats_(x, W, bias, h, None, 0, 2, h, planes)
+    torch.testing.assert_close(planes.double(), _planes_ref(h, P), rtol=2e-5, atol=2e-3)
+    # consumer: LN folded GEMM reading the planes
+    N = 2 * D
+    g = 1 + 0.2 * torch.randn(D, device=DEV)
+    be = 0.1 * torch.randn(D, device=DEV)
+    W2 = torch.randn(N, D, device=DEV) / D ** 0.5
+    b2 = 0.1 * torch.randn(N, device=DEV)
+    Wg = (W2 * g).to(torch.bfloat16)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    vpf().gemm(h, Wg, b2 + W2 @ be, None, None, 0, planes, Wg.float().sum(1), 4, out, P, 1e-6)
+    ref = Fn.layer_norm(h.double(), (D,), g.double(), be.double(), 1e-6) @ W2.double().t() + b2.double()
+    torch.testing.assert_close(out.double(), ref, rtol=2e-2, atol=3e-2)
+
+
+def test_patch_and_cls_stats_planes():
+    """EPI_PATCH + vpf_cls_rows_bf16 together fill the planes of every token row (patch rows by the GEMM, CLS
+    rows by cls_rows), matching the stored bf16 token rows."""
+    torch.manual_seed(5)
+    n, g2, D, K = 5, 196, 768, 768
+    P = 3
+    A = (torch.randn(n * g2, K, device=DEV) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(D, K, device=DEV) * 0.03).to(torch.bfloat16)
+    bias = torch.randn(D, device=DEV) * 0.1
+    pos = torch.randn(g2 + 1, D, device=DEV) * 0.1
+    cls = torch.randn(D, device=DEV)
+    tok = torch.empty(n, g2 + 1, D, device=DEV, dtype=torch.bfloat16)
+    planes = torch.full((P, n * (g2 + 1), 2), float("nan"), device=DEV)
+    vpf().gemm_stats_(A, W, bias, None, pos, g2, 3, tok, planes)
+    vpf().cls_rows_stats_(tok, cls, pos, planes)
+    ref = _planes_ref(tok.view(-1, D), P)
+    patch_rows = torch.ones(n * (g2 + 1), dtype=torch.bool)
+    patch_rows[:: g2 + 1] = False
+    torch.testing.assert_close(planes[:, patch_rows].double(), ref[:, patch_rows], rtol=2e-5, atol=2e-3)
+    # CLS rows: the whole row's {sum, sumsq} in plane 0, zeros elsewhere (the consumer sums the planes)
+    torch.testing.assert_close(planes[0, ~patch_rows].double(), ref[:, ~patch_rows].sum(0), rtol=2e-5, atol=2e-3)
+    assert torch.all(planes[1:, ~patch_rows] == 0)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_gemm_strided_rows(dtype):
     """a / out / residual as row-strided views (the last layer's CLS rows of the token tensor)."""

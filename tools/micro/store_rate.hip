@@ -30,8 +30,8 @@ int main() {
     void* buf; hipMalloc(&buf, bytes); hipMemset(buf, 0, bytes);
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     for (int kind = 0; kind < 2; ++kind)
-        for (int nwg : {8, 32, 128, 256, 2048}) {
-            for (int kbw : {16}) {   // KiB per wave: 16 -> 128 KiB per workgroup (one 256x256 bf16 tile)
+        for (int nwg : {1, 64, 256}) {
+            for (int kbw : {1, 4, 16, 64}) {   // KiB per wave: 16 -> 128 KiB per workgroup (one 256x256 bf16 tile)
                 const int per_wave = kind == 0 ? kbw : kbw * 2;
                 std::vector<float> t;
                 for (int r = 0; r < 20; ++r) {

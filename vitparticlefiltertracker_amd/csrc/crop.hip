@@ -218,13 +218,45 @@ __global__ __launch_bounds__(256) void k_cls_rows(T* __restrict__ tok, int64_t n
     else tok[p * (int64_t)N * D + d] = v;
 }
 
+// Stats-plane entries of the CLS rows (vpf_gemm_bf16 stats_out layout): every CLS row holds the same bf16
+// values bf16(cls + pos[0]), so one workgroup reduces {sum, sumsq} once and writes it to plane 0 of each
+// particle's CLS row (planes 1.. get 0: the consumer sums the planes).
+__global__ __launch_bounds__(256) void k_cls_stats(int64_t n_part, int N, int D, const float* __restrict__ cls,
+                                                   const float* __restrict__ pos, float2* __restrict__ st,
+                                                   int parts) {
+    __shared__ float red[2][4];
+    float s = 0.f, q = 0.f;
+    for (int d = threadIdx.x; d < D; d += 256) {
+        const float v = bf2f(f2bf(cls[d] + pos[d]));
+        s += v;
+        q = fmaf(v, v, q);
+    }
+    s = wave_sum(s);
+    q = wave_sum(q);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = s; red[1][w] = q; }
+    __syncthreads();
+    const float2 t = make_float2(red[0][0] + red[0][1] + red[0][2] + red[0][3],
+                                 red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    const int64_t rows = n_part * N;
+    for (int64_t p = threadIdx.x; p < n_part; p += 256)
+        for (int k = 0; k < parts; ++k) st[k * rows + p * N] = k == 0 ? t : make_float2(0.f, 0.f);
+}
+
 VPF_API int vpf_cls_rows_bf16(uint16_t* tokens, int64_t n_part, int N, int D, const float* cls,
-                              const float* pos, void* stream) {
+                              const float* pos, float* stats_out, int parts, void* stream) {
     if (n_part < 0 || N <= 0 || D <= 0) return VPF_ERR_ARG;
+    if (stats_out && (parts < 1 || parts > 4 || ((uintptr_t)stats_out & 7))) return VPF_ERR_ARG;
     if (n_part == 0) return 0;
     const unsigned blocks = (unsigned)((n_part * D + 255) / 256);
     hipLaunchKernelGGL(k_cls_rows<uint16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, tokens, n_part, N,
                        D, cls, pos);
+    if (stats_out) {
+        const int e = (int)hipGetLastError();
+        if (e) return e;
+        hipLaunchKernelGGL(k_cls_stats, dim3(1), dim3(256), 0, (hipStream_t)stream, n_part, N, D, cls, pos,
+                           reinterpret_cast<float2*>(stats_out), parts);
+    }
     VPF_RETURN_LAUNCH();
 }
 

@@ -35,7 +35,11 @@ constexpr int NTHREADS = 512;
 constexpr int OPERAND_BYTES = BM * BK * 2;      // 32 KiB per operand tile
 constexpr int STAGE_BYTES = 2 * OPERAND_BYTES;  // A + B
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KiB
-constexpr int AUX_BYTES = 4096;                 // epilogue operands: bias | colsum | row stats (1+1+2 KiB)
+// epilogue operands: bias (1 KiB) | colsum (1 KiB) | row statistics (up to VPF_MAX_STAT_PARTS planes of 2 KiB)
+// | producer per-row partial sums (256 rows x 4 waves x 8 B = 8 KiB)
+constexpr int MAX_PARTS = 4;
+constexpr int AUX_RED = 2048 + MAX_PARTS * 2048;
+constexpr int AUX_BYTES = AUX_RED + 8192;
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -56,11 +60,26 @@ __device__ __forceinline__ f32x2 gelu_sig2(f32x2 x) {
     return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
+// Sum of a float over the 8 consecutive lanes of each lane octet (DPP: quad swaps, then half-row mirror).
+__device__ __forceinline__ float octet_sum(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+    return v;
+}
+
+// Epilogue of one wave's 128 (M) x 64 (N) sub-tile. `img` is this wave's private 16 KiB of LDS (free of any
+// operand the other waves still read), `aux` the epilogue-operand region (bias | colsum at column offset
+// wn*64 of the tile, row statistics at row offset wm*128). Bias / LN-fold / GELU in fp32 on the
+// accumulators, bf16 pack, 8-B writes into an XOR-swizzled image, then 16-B coalesced row stores (+ residual
+// / position-embedding adds on the packed values). `red` (LDS, may be null): for the producers of the
+// residual stream (EPI_BIAS_RESIDUAL, EPI_PATCH) the per-row {sum, sumsq} of the stored bf16 values over the
+// wave's 64 columns, at red[(wm*128 + row) * 4 + wn] (float2), for the caller's per-tile combine.
 template <int EPI>
 __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
                                                 int m0, int n0, int lane, const bf16_t* residual,
                                                 const float* __restrict__ pos, int g2, bf16_t* C, int ldc, int M,
-                                                int N) {
+                                                int N, float2* red) {
     constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
     const int fr = lane & 15, fq = lane >> 4;
     float4 bv[4], cv[4];
@@ -117,6 +136,7 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
                                        : make_uint4(0, 0, 0, 0);
         }
     }
+    constexpr bool PROD = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH);
     __builtin_amdgcn_wave_barrier();   // the image is private to this wave: LDS ops of one wave stay in order
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
@@ -125,12 +145,12 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
         if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
         const int m = m0 + wm * 128 + row;
         const int n = n0 + wn * 64 + c16 * 8;
-        if (m >= M || n >= N) continue;
+        const bool ok = m < M && n < N;
         int64_t orow = m;
         if constexpr (EPI == VPF_EPI_PATCH) {
             const int pi = m % g2;
             orow = (int64_t)(m / g2) * (g2 + 1) + 1 + pi;
-            const float* pr = pos + (int64_t)(1 + pi) * N + n;
+            const float* pr = pos + (int64_t)(1 + pi) * N + min(n, N - 8);
             const float4 p0 = *reinterpret_cast<const float4*>(pr);
             const float4 p1 = *reinterpret_cast<const float4*>(pr + 4);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -152,7 +172,28 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
                                 bf2f((bf16_t)(w[e] >> 16)) + bf2f((bf16_t)(rr[e] >> 16)));
             v = make_uint4(o[0], o[1], o[2], o[3]);
         }
-        *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
+        if constexpr (PROD) {
+            if (red != nullptr) {   // wave-uniform
+                // {sum, sumsq} of the 8 stored values, then over the row's 8 lanes (64 columns)
+                // v_dot2_f32_bf16 on the packed pairs: sum = dot(w, (1, 1)), sumsq = dot(w, w) (bf16 products are
+                // exact in fp32)
+                typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                const bf16x2_t one2 = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, w[e]);
+                    s1 = __builtin_amdgcn_fdot2_f32_bf16(pr, one2, s1, false);
+                    s2 = __builtin_amdgcn_fdot2_f32_bf16(pr, pr, s2, false);
+                }
+                if (!ok) { s1 = 0.f; s2 = 0.f; }
+                s1 = octet_sum(s1);
+                s2 = octet_sum(s2);
+                if (c16 == 0) red[(wm * 128 + row) * 4 + wn] = make_float2(s1, s2);
+            }
+        }
+        if (ok) *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
     }
 }
 
@@ -164,12 +205,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                                                         const float* __restrict__ pos, int g2,
                                                         const float2* __restrict__ stats,
                                                         const float* __restrict__ colsum,
-                                                        bf16_t* C, int ldc, int M, int N, int K, int group) {
+                                                        bf16_t* C, int ldc, int M, int N, int K, int group,
+                                                        int stats_parts, float ln_eps, float* stats_out,
+                                                        int stats_rows) {
     // DEEP: A ring of 3 K-tiles (A prefetched 2 K-tiles ahead: the activation panel is the operand that
     // misses L2), B ring of 2 (weights stay L2-hot); 5 x 32 KiB = all 160 KiB of LDS, and the epilogue
     // operands go into the A slot no K-tile uses any more (slot nk % 3, DMA'd at K-tile max(nk-2, 0)).
     // !DEEP: the 2-stage A+B ring (2 x 64 KiB + 4 KiB aux), kept for A/B timing (vpf_gemm_tune).
     constexpr int SMEM = DEEP ? 5 * OPERAND_BYTES : LDS_BYTES + AUX_BYTES;
+    static_assert(AUX_BYTES <= OPERAND_BYTES, "aux region must fit the free A slot of the deep ring");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -263,9 +307,13 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             if (wid == 1)
                 __builtin_amdgcn_global_load_lds((gptr_t)(colsum + min(n0 + lane * 4, N - 4)), (lptr_t)(aux + 1024), 16,
                                                  0, 0);
+            // stats_parts == 0: one {mean, rstd} plane; else stats_parts {sum, sumsq} planes of M rows each
             const float* sd = reinterpret_cast<const float*>(stats);
-            __builtin_amdgcn_global_load_lds((gptr_t)(sd + min(2 * m0 + wid * 64 + lane, 2 * M - 1)),
-                                             (lptr_t)(aux + 2048 + wid * 256), 4, 0, 0);
+            const int planes = stats_parts > 0 ? stats_parts : 1;
+            for (int p = 0; p < planes; ++p)
+                __builtin_amdgcn_global_load_lds(
+                    (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + wid * 64 + lane, 2 * M - 1)),
+                    (lptr_t)(aux + 2048 + p * 2048 + wid * 256), 4, 0, 0);
         }
     };
     if constexpr (!DEEP) {
@@ -321,14 +369,49 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     }
 
     // ---------------- epilogue ----------------
+    if constexpr (LN) {
+        // statistics planes -> {mean, rstd} once per row (in place over plane 0, which only this thread
+        // reads), instead of in each of the 4 waves that share the row; the aux DMA landed before the last
+        // K-step's barrier
+        if (stats_parts > 0 && tid < BM) {
+            float sm = 0.f, sq = 0.f;
+            for (int p = 0; p < stats_parts; ++p) {
+                const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + p * 2048 + tid * 8);
+                sm += st.x;
+                sq += st.y;
+            }
+            const float inv_k = 1.0f / (float)K;
+            const float mean = sm * inv_k;
+            const float var = fmaxf(fmaf(sq, inv_k, -mean * mean), 0.f);
+            *reinterpret_cast<float2*>(aux + 2048 + tid * 8) = make_float2(mean, __builtin_amdgcn_rsqf(var + ln_eps));
+        }
+    }
     __syncthreads();   // every wave is done with the operand ring; reuse it as 8 x 16 KiB images
     char* img = smem + wid * 16384;
     if constexpr (DEEP) {   // the four 32 KiB slots other than the aux slot
         const int region = (wid >> 1) + ((wid >> 1) >= (nk % 3) ? 1 : 0);
         img = smem + region * OPERAND_BYTES + (wid & 1) * 16384;
     }
-    store_wave_tile<EPI>(img, aux, acc, wm, wn, m0, n0, lane, residual, pos, g2, C, ldc,
-                         M, N);
+    float2* red = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) && stats_out != nullptr
+                      ? reinterpret_cast<float2*>(aux + AUX_RED) : nullptr;
+    store_wave_tile<EPI>(img, aux, acc, wm, wn, m0, n0, lane, residual, pos, g2, C, ldc, M, N, red);
+    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) {
+        if (stats_out != nullptr) {
+            // the tile's {sum, sumsq} per row over its (up to) 256 columns -> plane tn, row = output row
+            __syncthreads();
+            if (tid < BM) {
+                const int m = m0 + tid;
+                if (m < M) {
+                    float2 t = red[tid * 4];
+#pragma unroll
+                    for (int w = 1; w < 4; ++w) { const float2 u = red[tid * 4 + w]; t.x += u.x; t.y += u.y; }
+                    int64_t orow = m;
+                    if constexpr (EPI == VPF_EPI_PATCH) orow = (int64_t)(m / g2) * (g2 + 1) + 1 + m % g2;
+                    reinterpret_cast<float2*>(stats_out)[(int64_t)tn * stats_rows + orow] = t;
+                }
+            }
+        }
+    }
 }
 
 }  // namespace
@@ -338,11 +421,11 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         if (kern == 2)                                                                                       \
             hipLaunchKernelGGL((k_gemm_bf16<E, false>), grid, block, 0, s, A, (int)lda, W, bias, residual, pos, \
                                patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, \
-                               k, group);                                                                    \
+                               k, group, stats_parts, ln_eps, stats_out, stats_rows);                        \
         else                                                                                                 \
             hipLaunchKernelGGL((k_gemm_bf16<E, true>), grid, block, 0, s, A, (int)lda, W, bias, residual, pos,  \
                                patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, \
-                               k, group);                                                                    \
+                               k, group, stats_parts, ln_eps, stats_out, stats_rows);                        \
     } while (0)
 
 static int g_group = -1;
@@ -369,7 +452,7 @@ VPF_API int vpf_gemm_tune(int kernel, int group) {
 VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, const float* bias,
                           const uint16_t* residual, const float* pos, int patch_rows, const float* row_stats,
                           const float* colsum, uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                          int epilogue, void* stream) {
+                          int epilogue, int stats_parts, float ln_eps, float* stats_out, void* stream) {
     if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 8 != 0 || lda < K || lda % 8 != 0 || ldc < N ||
         ldc % 8 != 0)
         return VPF_ERR_ARG;
@@ -381,6 +464,13 @@ VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, con
     if ((epilogue == VPF_EPI_LN || epilogue == VPF_EPI_LN_GELU) && (!row_stats || !colsum)) return VPF_ERR_ARG;
     // bias / colsum are DMA'd in 16-B pieces, row stats in 4-B pieces
     if (((uintptr_t)bias & 15) || ((uintptr_t)colsum & 15) || ((uintptr_t)row_stats & 7)) return VPF_ERR_ARG;
+    if (stats_parts < 0 || stats_parts > MAX_PARTS || !(ln_eps >= 0.f)) return VPF_ERR_ARG;
+    if (stats_out && (((uintptr_t)stats_out & 7) || (epilogue != VPF_EPI_BIAS_RESIDUAL && epilogue != VPF_EPI_PATCH)))
+        return VPF_ERR_ARG;
+    // producer plane stride: rows of C (EPI_PATCH interleaves one CLS row per patch_rows rows)
+    const int64_t srows = epilogue == VPF_EPI_PATCH ? (M / patch_rows) * (patch_rows + 1) : M;
+    if (srows > INT32_MAX) return VPF_ERR_ARG;
+    const int stats_rows = (int)srows;
     const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     if (tiles > INT32_MAX) return VPF_ERR_ARG;
     hipStream_t s = (hipStream_t)stream;

@@ -75,8 +75,23 @@ def cls_rows_(tokens: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor) -> Non
     """H3: tokens[p][0][:] = cls + pos[0]; tokens [n][N][D]."""
     _dev(tokens, cls, pos)
     n, N, D = tokens.shape
-    name = "vpf_cls_rows_bf16" if tokens.dtype == _BF16 else "vpf_cls_rows_f32"
-    call(name, ptr(tokens), n, N, D, ptr(cls), ptr(pos), stream_ptr())
+    if tokens.dtype == _BF16:
+        call("vpf_cls_rows_bf16", ptr(tokens), n, N, D, ptr(cls), ptr(pos), None, 0, stream_ptr())
+    else:
+        call("vpf_cls_rows_f32", ptr(tokens), n, N, D, ptr(cls), ptr(pos), stream_ptr())
+
+
+@torch.library.custom_op("vpf::cls_rows_stats_", mutates_args={"tokens", "stats_out"}, device_types="cuda")
+def cls_rows_stats_(tokens: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor, stats_out: torch.Tensor) -> None:
+    """cls_rows_ (bf16) that also writes the CLS rows' {sum, sumsq} into the residual-stream statistics planes
+    `stats_out` [P][n*N][2] f32 (plane 0; other planes 0), the layout vpf_gemm_bf16 producers write."""
+    _dev(tokens, cls, pos, stats_out)
+    n, N, D = tokens.shape
+    _chk(tokens.dtype == _BF16, "cls_rows_stats_: bf16 tokens")
+    _chk(stats_out.dtype == _F32 and stats_out.dim() == 3 and tuple(stats_out.shape[1:]) == (n * N, 2),
+         "cls_rows_stats_: stats_out f32[P][n*N][2]")
+    call("vpf_cls_rows_bf16", ptr(tokens), n, N, D, ptr(cls), ptr(pos), ptr(stats_out), stats_out.shape[0],
+         stream_ptr())
 
 
 def _rows(t: torch.Tensor, what: str):
@@ -85,15 +100,8 @@ def _rows(t: torch.Tensor, what: str):
     return t.shape[0], t.stride(0)
 
 
-@torch.library.custom_op("vpf::gemm", mutates_args={"out"}, device_types="cuda")
-def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: Optional[torch.Tensor],
-         pos: Optional[torch.Tensor], patch_rows: int, row_stats: Optional[torch.Tensor],
-         colsum: Optional[torch.Tensor], epilogue: int, out: torch.Tensor) -> None:
-    """H3/H5/H7/H8: out = epilogue(a[M][K] . w[N][K]^T) (bf16 MFMA or fp32 parity mode by dtype).
-
-    `a`, `out` (and `residual`, which must share `out`'s row stride) are 2-D views whose rows may be strided
-    (e.g. the CLS rows of the token tensor). EPI_PATCH takes `out` as the flat token buffer."""
-    _dev(w, bias, pos, row_stats, colsum)
+def _gemm(a, w, bias, residual, pos, patch_rows, row_stats, colsum, epilogue, out, stats_parts, ln_eps, stats_out):
+    _dev(w, bias, pos, row_stats, colsum, stats_out)
     for t in (a, out, residual):
         if t is not None:
             _chk(t.is_cuda, "vpf ops run on the GPU only (no CPU fallback); got a CPU tensor")
@@ -112,11 +120,44 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: Optiona
     if residual is not None:
         _chk(_rows(residual, "gemm residual") == (M, ldc), "gemm: residual must match out's layout")
     if epilogue in (_lib.VPF_EPI_LN, _lib.VPF_EPI_LN_GELU):
-        _chk(row_stats is not None and row_stats.numel() >= 2 * M and colsum is not None and colsum.numel() == N,
-             "gemm: LN epilogue needs row_stats[M][2] and colsum[N]")
-    name = "vpf_gemm_bf16" if a.dtype == _BF16 else "vpf_gemm_f32"
-    call(name, ptr(a), lda, ptr(w), ptr(bias), ptr(residual), ptr(pos), patch_rows, ptr(row_stats), ptr(colsum),
-         ptr(out), ldc, M, N, K, epilogue, stream_ptr())
+        _chk(row_stats is not None and row_stats.numel() >= 2 * M * max(stats_parts, 1) and colsum is not None
+             and colsum.numel() == N, "gemm: LN epilogue needs row_stats [max(P,1)][M][2] and colsum[N]")
+    if a.dtype == _BF16:
+        if stats_out is not None:
+            R = (M // patch_rows) * (patch_rows + 1) if epilogue == _lib.VPF_EPI_PATCH else M
+            _chk(stats_out.dtype == _F32 and stats_out.numel() >= ((N + 255) // 256) * R * 2,
+                 "gemm: stats_out f32[ceil(N/256)][rows][2]")
+        call("vpf_gemm_bf16", ptr(a), lda, ptr(w), ptr(bias), ptr(residual), ptr(pos), patch_rows, ptr(row_stats),
+             ptr(colsum), ptr(out), ldc, M, N, K, epilogue, stats_parts, ln_eps, ptr(stats_out), stream_ptr())
+    else:
+        _chk(stats_parts == 0 and stats_out is None, "gemm: statistics planes are a bf16-path feature")
+        call("vpf_gemm_f32", ptr(a), lda, ptr(w), ptr(bias), ptr(residual), ptr(pos), patch_rows, ptr(row_stats),
+             ptr(colsum), ptr(out), ldc, M, N, K, epilogue, stream_ptr())
+
+
+@torch.library.custom_op("vpf::gemm", mutates_args={"out"}, device_types="cuda")
+def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: Optional[torch.Tensor],
+         pos: Optional[torch.Tensor], patch_rows: int, row_stats: Optional[torch.Tensor],
+         colsum: Optional[torch.Tensor], epilogue: int, out: torch.Tensor, stats_parts: int = 0,
+         ln_eps: float = 0.0) -> None:
+    """H3/H5/H7/H8: out = epilogue(a[M][K] . w[N][K]^T) (bf16 MFMA or fp32 parity mode by dtype).
+
+    `a`, `out` (and `residual`, which must share `out`'s row stride) are 2-D views whose rows may be strided
+    (e.g. the CLS rows of the token tensor). EPI_PATCH takes `out` as the flat token buffer.
+    bf16 LN epilogues: `stats_parts` = 0 reads `row_stats` as {mean, rstd} rows (vpf_row_stats); P > 0 reads it
+    as P residual-stream statistics planes [P][M][2] of {sum, sumsq} (written by gemm_stats_ / cls_rows_stats_)
+    combined with `ln_eps`."""
+    _gemm(a, w, bias, residual, pos, patch_rows, row_stats, colsum, epilogue, out, stats_parts, ln_eps, None)
+
+
+@torch.library.custom_op("vpf::gemm_stats_", mutates_args={"out", "stats_out"}, device_types="cuda")
+def gemm_stats_(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: Optional[torch.Tensor],
+                pos: Optional[torch.Tensor], patch_rows: int, epilogue: int, out: torch.Tensor,
+                stats_out: torch.Tensor) -> None:
+    """gemm (bf16, EPI_BIAS_RESIDUAL / EPI_PATCH) that also writes the residual-stream statistics planes of its
+    output: `stats_out` [ceil(N/256)][rows][2] f32, per row {sum, sumsq} of the stored bf16 values over each
+    256-column block (rows = output rows; token rows for EPI_PATCH, whose CLS rows cls_rows_stats_ fills)."""
+    _gemm(a, w, bias, residual, pos, patch_rows, None, None, epilogue, out, 0, 0.0, stats_out)
 
 
 @torch.library.custom_op("vpf::row_stats", mutates_args={"out"}, device_types="cuda")

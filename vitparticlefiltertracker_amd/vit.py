@@ -151,6 +151,11 @@ class ViTEngine:
         self.hid = self.hid_flat[: n * N * F].view(n * N, F)
         self.patches = self.hid_flat[: n * A.n_patches * A.patch_kp].view(n * A.n_patches, A.patch_kp)
         self.stats = torch.empty(n * N, 2, device=dev, dtype=torch.float32)
+        # bf16 fold mode: residual-stream statistics planes written by the GEMMs that produce h (patch embed,
+        # proj, fc2) and read by the LN-folded GEMMs (qkv, fc1): [P][rows][2] {sum, sumsq} per 256-column block
+        self.parts = (D + 255) // 256
+        self.planes_flat = torch.empty(self.parts * n * N * 2, device=dev, dtype=torch.float32)
+        self.planes_cls_flat = torch.empty(self.parts * n * 2, device=dev, dtype=torch.float32)
         self.Q = torch.empty(n, device=dev, dtype=torch.int64)
         self.feat = torch.empty(n, D, device=dev, dtype=torch.float32)
         self.sim = torch.empty(n, device=dev, dtype=torch.float32)
@@ -168,9 +173,20 @@ class ViTEngine:
         _run(T, "crop_patches", vpf.crop_patches, frame, self.rgba, particles, [float(box_wh[0]), float(box_wh[1])],
              A.img_size, A.patch, self.norm_ab, patches)
         h = self.h[:n]
-        _run(T, "gemm_patch", vpf.gemm, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches, None, None,
-             _lib.VPF_EPI_PATCH, h)
-        _run(T, "cls_rows", vpf.cls_rows_, h, self.cls, self.pos)
+        pl = self.planes(n) if self.fold_ln else None
+        if pl is not None:
+            _run(T, "gemm_patch", vpf.gemm_stats_, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches,
+                 _lib.VPF_EPI_PATCH, h, pl)
+            _run(T, "cls_rows", vpf.cls_rows_stats_, h, self.cls, self.pos, pl)
+        else:
+            _run(T, "gemm_patch", vpf.gemm, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches, None, None,
+                 _lib.VPF_EPI_PATCH, h)
+            _run(T, "cls_rows", vpf.cls_rows_, h, self.cls, self.pos)
+
+    def planes(self, n: int) -> torch.Tensor:
+        """Statistics planes of h[:n] (plane stride n*N rows, as the producing GEMMs write them)."""
+        N = self.arch.tokens
+        return self.planes_flat[: self.parts * n * N * 2].view(self.parts, n * N, 2)
 
     def encoder(self, n: int) -> None:
         """L pre-norm blocks on h[:n]. The last block only needs the CLS rows after its attention (the
@@ -192,8 +208,9 @@ class ViTEngine:
         BIAS, GELU, RES = _lib.VPF_EPI_BIAS, _lib.VPF_EPI_BIAS_GELU, _lib.VPF_EPI_BIAS_RESIDUAL
         LNE, LNG = _lib.VPF_EPI_LN, _lib.VPF_EPI_LN_GELU
         fold = self.fold_ln
-        if fold:
-            _run(T, "row_stats", vpf.row_stats, h2, A.ln_eps, st)
+        P, eps = self.parts, A.ln_eps
+        pl = self.planes(n) if fold else None                  # planes of h2 (written by embed / proj / fc2)
+        plc = self.planes_cls_flat[: P * n * 2].view(P, n, 2)  # planes of the last block's CLS rows
         q2 = qkv.view(n * N, 3 * D)
         kv2 = q2[:, D:]                                 # K | V columns of every row
         qc = qkv.view(n, N * 3 * D)[:, :D]             # Q columns of the CLS rows
@@ -202,11 +219,12 @@ class ViTEngine:
             # the last block's attention reads only the CLS query: K, V for every row, Q for the CLS rows
             if fold:
                 if not last:
-                    _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, st, L["cqkv"], LNE, q2)
+                    _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, pl, L["cqkv"], LNE, q2,
+                         P, eps)
                 else:
-                    _run(T, "gemm_kv", vpf.gemm, h2, L["wqkv"][D:], L["bqkv"][D:], None, None, 0, st, L["cqkv"][D:],
-                         LNE, kv2)
-                    _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # st already consumed above
+                    _run(T, "gemm_kv", vpf.gemm, h2, L["wqkv"][D:], L["bqkv"][D:], None, None, 0, pl, L["cqkv"][D:],
+                         LNE, kv2, P, eps)
+                    _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # the CLS rows' {mean, rstd}
                     _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc,
                          L["cqkv"][:D], LNE, qc)
             else:
@@ -219,18 +237,21 @@ class ViTEngine:
                     _run(T, "gemm_q_cls", vpf.gemm, xc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, None, None,
                          BIAS, qc)
             _run(T, "attention_cls" if last else "attention", vpf.attention, qkv, A.heads, 1 if last else N, self.x[:n])
-            hh, xx, hd_, ss = (hc, xc, hidc, stc) if last else (h2, x2, hid, st)
+            hh, xx, hd_, pp = (hc, xc, hidc, plc) if last else (h2, x2, hid, pl)
             tag = "_cls" if last else ""
-            _run(T, "gemm_proj" + tag, vpf.gemm, xx, L["wproj"], L["bproj"], hh, None, 0, None, None, RES, hh)
             if fold:
-                _run(T, "row_stats", vpf.row_stats, hh, A.ln_eps, ss)
-                _run(T, "gemm_fc1" + tag, vpf.gemm, hh, L["wfc1"], L["bfc1"], None, None, 0, ss, L["cfc1"], LNG, hd_)
+                _run(T, "gemm_proj" + tag, vpf.gemm_stats_, xx, L["wproj"], L["bproj"], hh, None, 0, RES, hh, pp)
+                _run(T, "gemm_fc1" + tag, vpf.gemm, hh, L["wfc1"], L["bfc1"], None, None, 0, pp, L["cfc1"], LNG, hd_,
+                     P, eps)
+                if not last:
+                    _run(T, "gemm_fc2" + tag, vpf.gemm_stats_, hd_, L["wfc2"], L["bfc2"], hh, None, 0, RES, hh, pl)
+                else:   # the last block's output only feeds the final LayerNorm (cls_weight computes its stats)
+                    _run(T, "gemm_fc2" + tag, vpf.gemm, hd_, L["wfc2"], L["bfc2"], hh, None, 0, None, None, RES, hh)
             else:
+                _run(T, "gemm_proj" + tag, vpf.gemm, xx, L["wproj"], L["bproj"], hh, None, 0, None, None, RES, hh)
                 _run(T, "layernorm", vpf.layernorm, hh, L["n2g"], L["n2b"], A.ln_eps, xx)
                 _run(T, "gemm_fc1" + tag, vpf.gemm, xx, L["wfc1"], L["bfc1"], None, None, 0, None, None, GELU, hd_)
-            _run(T, "gemm_fc2" + tag, vpf.gemm, hd_, L["wfc2"], L["bfc2"], hh, None, 0, None, None, RES, hh)
-            if fold and not last:
-                _run(T, "row_stats", vpf.row_stats, h2, A.ln_eps, st)
+                _run(T, "gemm_fc2" + tag, vpf.gemm, hd_, L["wfc2"], L["bfc2"], hh, None, 0, None, None, RES, hh)
 
     def weights_from_tokens(self, n: int, tmpl: torch.Tensor, lam: float, bits: int, want_feat: bool = False):
         _run(self.timer, "cls_weight", vpf.cls_weight, self.h[:n], self.ng, self.nb, self.arch.ln_eps, tmpl,
