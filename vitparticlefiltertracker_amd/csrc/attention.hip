@@ -321,16 +321,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     if (!active) return;
     l += __shfl_xor(l, 32, 64);
     const float inv = 1.0f / l;
-    if (q < q_rows) {
-        bf16_t* orow = out + (row0 + q) * D + h * HD;
+    // Lane (l32, hh) holds dims 8k + 4hh .. +3 of query l32 for the eight 8-dim groups k (o0: k < 4, o1: k >= 4).
+    // v_permlane32_swap per pair (k, k+1) gives the lower half-wave dims 8k..8k+7 and the upper half-wave
+    // 8k+8..8k+15: one 16-B store per pair (cdna_hip_programming.md T21) instead of two 8-B stores.
+    uint32_t gx[8], gy[8];
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            const int d = 8 * g4 + 4 * hh;
-            *reinterpret_cast<uint2*>(orow + d) =
-                make_uint2(pack_bf2(o0[4 * g4] * inv, o0[4 * g4 + 1] * inv), pack_bf2(o0[4 * g4 + 2] * inv, o0[4 * g4 + 3] * inv));
-            *reinterpret_cast<uint2*>(orow + 32 + d) =
-                make_uint2(pack_bf2(o1[4 * g4] * inv, o1[4 * g4 + 1] * inv), pack_bf2(o1[4 * g4 + 2] * inv, o1[4 * g4 + 3] * inv));
-        }
+    for (int k = 0; k < 8; ++k) {
+        const f32x16& o = k < 4 ? o0 : o1;
+        const int b4 = 4 * (k & 3);
+        gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
+        gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
+    }
+    uint4 ov[4];
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {   // all lanes active: the swaps read the partner half-wave
+        const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
+        ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
+    if (q < q_rows) {
+        bf16_t* orow = out + (row0 + q) * D + h * HD + 8 * hh;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
     }
 }
 
