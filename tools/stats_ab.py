@@ -22,7 +22,7 @@ b1 = torch.zeros(F, device=dev)
 c1 = W1.float().sum(1)
 hid = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
 st = torch.empty(M, 2, device=dev)
-planes = torch.empty(3, M, 2, device=dev)
+planes = torch.empty(12, M, 2, device=dev)
 RES, LNG = _lib.VPF_EPI_BIAS_RESIDUAL, _lib.VPF_EPI_LN_GELU
 
 
@@ -34,7 +34,7 @@ def old():
 
 def new():
     vpf.gemm_stats_(x, Wp, bp, h, None, 0, RES, h, planes)
-    vpf.gemm(h, W1, b1, None, None, 0, planes, c1, LNG, hid, 3, 1e-6)
+    vpf.gemm(h, W1, b1, None, None, 0, planes, c1, LNG, hid, 12, 1e-6)
 
 
 parts = {
@@ -42,7 +42,7 @@ parts = {
     "proj+stats_out": lambda: vpf.gemm_stats_(x, Wp, bp, h, None, 0, RES, h, planes),
     "row_stats": lambda: vpf.row_stats(h, 1e-6, st),
     "fc1 P=0": lambda: vpf.gemm(h, W1, b1, None, None, 0, st, c1, LNG, hid),
-    "fc1 P=3": lambda: vpf.gemm(h, W1, b1, None, None, 0, planes, c1, LNG, hid, 3, 1e-6),
+    "fc1 P=12": lambda: vpf.gemm(h, W1, b1, None, None, 0, planes, c1, LNG, hid, 12, 1e-6),
     "old chain": old,
     "new chain": new,
 }

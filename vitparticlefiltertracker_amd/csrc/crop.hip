@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void k_cls_stats(int64_t n_part, int N, int D,
 VPF_API int vpf_cls_rows_bf16(uint16_t* tokens, int64_t n_part, int N, int D, const float* cls,
                               const float* pos, float* stats_out, int parts, void* stream) {
     if (n_part < 0 || N <= 0 || D <= 0) return VPF_ERR_ARG;
-    if (stats_out && (parts < 1 || parts > 4 || ((uintptr_t)stats_out & 7))) return VPF_ERR_ARG;
+    if (stats_out && (parts < 1 || parts > 64 || ((uintptr_t)stats_out & 7))) return VPF_ERR_ARG;
     if (n_part == 0) return 0;
     const unsigned blocks = (unsigned)((n_part * D + 255) / 256);
     hipLaunchKernelGGL(k_cls_rows<uint16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, tokens, n_part, N,

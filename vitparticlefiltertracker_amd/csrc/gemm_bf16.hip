@@ -35,11 +35,11 @@ constexpr int NTHREADS = 512;
 constexpr int OPERAND_BYTES = BM * BK * 2;      // 32 KiB per operand tile
 constexpr int STAGE_BYTES = 2 * OPERAND_BYTES;  // A + B
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KiB
-// epilogue operands: bias (1 KiB) | colsum (1 KiB) | row statistics (up to VPF_MAX_STAT_PARTS planes of 2 KiB)
-// | producer per-row partial sums (256 rows x 4 waves x 8 B = 8 KiB)
-constexpr int MAX_PARTS = 4;
-constexpr int AUX_RED = 2048 + MAX_PARTS * 2048;
-constexpr int AUX_BYTES = AUX_RED + 8192;
+// epilogue operands: bias (1 KiB) | colsum (1 KiB) | row statistics (up to MAX_PARTS planes of 2 KiB)
+// (consumers) or the producers' per-wave row partials (8 x 128 rows x 8 B) at 2 KiB
+constexpr int MAX_PARTS = 15;
+constexpr int AUX_RED = 2048;
+constexpr int AUX_BYTES = 2048 + MAX_PARTS * 2048;
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -72,14 +72,15 @@ __device__ __forceinline__ float octet_sum(float v) {
 // operand the other waves still read), `aux` the epilogue-operand region (bias | colsum at column offset
 // wn*64 of the tile, row statistics at row offset wm*128). Bias / LN-fold / GELU in fp32 on the
 // accumulators, bf16 pack, 8-B writes into an XOR-swizzled image, then 16-B coalesced row stores (+ residual
-// / position-embedding adds on the packed values). `red` (LDS, may be null): for the producers of the
+// / position-embedding adds on the packed values). `stats_out` (may be null): for the producers of the
 // residual stream (EPI_BIAS_RESIDUAL, EPI_PATCH) the per-row {sum, sumsq} of the stored bf16 values over the
-// wave's 64 columns, at red[(wm*128 + row) * 4 + wn] (float2), for the caller's per-tile combine.
+// wave's 64 columns go to plane n0/64 + wn (plane stride stats_rows rows), staged through the wave's 1 KiB
+// of `red` (LDS) so that each lane stores two rows with one 16-B store; no cross-wave step.
 template <int EPI>
 __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
                                                 int m0, int n0, int lane, const bf16_t* residual,
                                                 const float* __restrict__ pos, int g2, bf16_t* C, int ldc, int M,
-                                                int N, float2* red) {
+                                                int N, float2* red, float* stats_out, int stats_rows) {
     constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
     const int fr = lane & 15, fq = lane >> 4;
     float4 bv[4], cv[4];
@@ -190,10 +191,32 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
                 if (!ok) { s1 = 0.f; s2 = 0.f; }
                 s1 = octet_sum(s1);
                 s2 = octet_sum(s2);
-                if (c16 == 0) red[(wm * 128 + row) * 4 + wn] = make_float2(s1, s2);
+                if (c16 == 0) red[row] = make_float2(s1, s2);
             }
         }
         if (ok) *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
+    }
+    if constexpr (PROD) {
+        const int nb = n0 + wn * 64;
+        if (red != nullptr && nb < N) {   // wave-uniform
+            __builtin_amdgcn_wave_barrier();
+            const float4 t = *reinterpret_cast<const float4*>(red + 2 * lane);   // rows 2*lane, 2*lane+1
+            float* plane = stats_out + (int64_t)(nb >> 6) * stats_rows * 2;
+            const int m = m0 + wm * 128 + 2 * lane;
+            if constexpr (EPI == VPF_EPI_PATCH) {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int me = m + e;
+                    if (me < M) {
+                        const int64_t orow = (int64_t)(me / g2) * (g2 + 1) + 1 + me % g2;
+                        *reinterpret_cast<float2*>(plane + orow * 2) = e ? make_float2(t.z, t.w) : make_float2(t.x, t.y);
+                    }
+                }
+            } else {
+                if (m + 1 < M) *reinterpret_cast<float4*>(plane + (int64_t)m * 2) = t;
+                else if (m < M) *reinterpret_cast<float2*>(plane + (int64_t)m * 2) = make_float2(t.x, t.y);
+            }
+        }
     }
 }
 
@@ -213,7 +236,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     // operands go into the A slot no K-tile uses any more (slot nk % 3, DMA'd at K-tile max(nk-2, 0)).
     // !DEEP: the 2-stage A+B ring (2 x 64 KiB + 4 KiB aux), kept for A/B timing (vpf_gemm_tune).
     constexpr int SMEM = DEEP ? 5 * OPERAND_BYTES : LDS_BYTES + AUX_BYTES;
-    static_assert(AUX_BYTES <= OPERAND_BYTES, "aux region must fit the free A slot of the deep ring");
+    static_assert(AUX_BYTES <= OPERAND_BYTES && AUX_RED + 8 * 1024 <= AUX_BYTES,
+                  "aux region must fit the free A slot of the deep ring");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -393,25 +417,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         img = smem + region * OPERAND_BYTES + (wid & 1) * 16384;
     }
     float2* red = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) && stats_out != nullptr
-                      ? reinterpret_cast<float2*>(aux + AUX_RED) : nullptr;
-    store_wave_tile<EPI>(img, aux, acc, wm, wn, m0, n0, lane, residual, pos, g2, C, ldc, M, N, red);
-    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) {
-        if (stats_out != nullptr) {
-            // the tile's {sum, sumsq} per row over its (up to) 256 columns -> plane tn, row = output row
-            __syncthreads();
-            if (tid < BM) {
-                const int m = m0 + tid;
-                if (m < M) {
-                    float2 t = red[tid * 4];
-#pragma unroll
-                    for (int w = 1; w < 4; ++w) { const float2 u = red[tid * 4 + w]; t.x += u.x; t.y += u.y; }
-                    int64_t orow = m;
-                    if constexpr (EPI == VPF_EPI_PATCH) orow = (int64_t)(m / g2) * (g2 + 1) + 1 + m % g2;
-                    reinterpret_cast<float2*>(stats_out)[(int64_t)tn * stats_rows + orow] = t;
-                }
-            }
-        }
-    }
+                      ? reinterpret_cast<float2*>(aux + AUX_RED) + wid * 128 : nullptr;
+    store_wave_tile<EPI>(img, aux, acc, wm, wn, m0, n0, lane, residual, pos, g2, C, ldc, M, N, red, stats_out,
+                         stats_rows);
 }
 
 }  // namespace

@@ -125,8 +125,8 @@ def _gemm(a, w, bias, residual, pos, patch_rows, row_stats, colsum, epilogue, ou
     if a.dtype == _BF16:
         if stats_out is not None:
             R = (M // patch_rows) * (patch_rows + 1) if epilogue == _lib.VPF_EPI_PATCH else M
-            _chk(stats_out.dtype == _F32 and stats_out.numel() >= ((N + 255) // 256) * R * 2,
-                 "gemm: stats_out f32[ceil(N/256)][rows][2]")
+            _chk(stats_out.dtype == _F32 and stats_out.numel() >= ((N + 63) // 64) * R * 2,
+                 "gemm: stats_out f32[ceil(N/64)][rows][2]")
         call("vpf_gemm_bf16", ptr(a), lda, ptr(w), ptr(bias), ptr(residual), ptr(pos), patch_rows, ptr(row_stats),
              ptr(colsum), ptr(out), ldc, M, N, K, epilogue, stats_parts, ln_eps, ptr(stats_out), stream_ptr())
     else:
@@ -155,8 +155,8 @@ def gemm_stats_(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: 
                 pos: Optional[torch.Tensor], patch_rows: int, epilogue: int, out: torch.Tensor,
                 stats_out: torch.Tensor) -> None:
     """gemm (bf16, EPI_BIAS_RESIDUAL / EPI_PATCH) that also writes the residual-stream statistics planes of its
-    output: `stats_out` [ceil(N/256)][rows][2] f32, per row {sum, sumsq} of the stored bf16 values over each
-    256-column block (rows = output rows; token rows for EPI_PATCH, whose CLS rows cls_rows_stats_ fills)."""
+    output: `stats_out` [ceil(N/64)][rows][2] f32, per row {sum, sumsq} of the stored bf16 values over each
+    64-column block (rows = output rows; token rows for EPI_PATCH, whose CLS rows cls_rows_stats_ fills)."""
     _gemm(a, w, bias, residual, pos, patch_rows, None, None, epilogue, out, 0, 0.0, stats_out)
 
 

@@ -152,8 +152,10 @@ class ViTEngine:
         self.patches = self.hid_flat[: n * A.n_patches * A.patch_kp].view(n * A.n_patches, A.patch_kp)
         self.stats = torch.empty(n * N, 2, device=dev, dtype=torch.float32)
         # bf16 fold mode: residual-stream statistics planes written by the GEMMs that produce h (patch embed,
-        # proj, fc2) and read by the LN-folded GEMMs (qkv, fc1): [P][rows][2] {sum, sumsq} per 256-column block
-        self.parts = (D + 255) // 256
+        # proj, fc2) and read by the LN-folded GEMMs (qkv, fc1): [P][rows][2] {sum, sumsq} per 64-column block.
+        # P <= 15 (the consumer's LDS copy); wider models (ViT-L, D = 1024) keep the row_stats pass.
+        self.parts = (D + 63) // 64
+        self.use_planes = self.fold_ln and self.parts <= 15
         self.planes_flat = torch.empty(self.parts * n * N * 2, device=dev, dtype=torch.float32)
         self.planes_cls_flat = torch.empty(self.parts * n * 2, device=dev, dtype=torch.float32)
         self.Q = torch.empty(n, device=dev, dtype=torch.int64)
@@ -173,7 +175,7 @@ class ViTEngine:
         _run(T, "crop_patches", vpf.crop_patches, frame, self.rgba, particles, [float(box_wh[0]), float(box_wh[1])],
              A.img_size, A.patch, self.norm_ab, patches)
         h = self.h[:n]
-        pl = self.planes(n) if self.fold_ln else None
+        pl = self.planes(n) if self.use_planes else None
         if pl is not None:
             _run(T, "gemm_patch", vpf.gemm_stats_, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches,
                  _lib.VPF_EPI_PATCH, h, pl)
@@ -207,10 +209,25 @@ class ViTEngine:
         stc = self.stats[:n]
         BIAS, GELU, RES = _lib.VPF_EPI_BIAS, _lib.VPF_EPI_BIAS_GELU, _lib.VPF_EPI_BIAS_RESIDUAL
         LNE, LNG = _lib.VPF_EPI_LN, _lib.VPF_EPI_LN_GELU
-        fold = self.fold_ln
+        fold, planes = self.fold_ln, self.use_planes
         P, eps = self.parts, A.ln_eps
-        pl = self.planes(n) if fold else None                  # planes of h2 (written by embed / proj / fc2)
+        pl = self.planes(n) if planes else None                # planes of h2 (written by embed / proj / fc2)
         plc = self.planes_cls_flat[: P * n * 2].view(P, n, 2)  # planes of the last block's CLS rows
+
+        def ln_stats(x, st_rows, pln):
+            """LayerNorm statistics of rows x for an LN-folded GEMM: the producer's planes, or a row_stats pass."""
+            if planes:
+                return pln, P
+            _run(T, "row_stats", vpf.row_stats, x, eps, st_rows)
+            return st_rows, 0
+
+        def residual_gemm(name, a, w, b, hh_, pln):
+            """h += a w^T + b, also writing h's statistics planes when the consumers read them."""
+            if planes and pln is not None:
+                _run(T, name, vpf.gemm_stats_, a, w, b, hh_, None, 0, RES, hh_, pln)
+            else:
+                _run(T, name, vpf.gemm, a, w, b, hh_, None, 0, None, None, RES, hh_)
+
         q2 = qkv.view(n * N, 3 * D)
         kv2 = q2[:, D:]                                 # K | V columns of every row
         qc = qkv.view(n, N * 3 * D)[:, :D]             # Q columns of the CLS rows
@@ -218,12 +235,13 @@ class ViTEngine:
             last = l == len(self.layers) - 1
             # the last block's attention reads only the CLS query: K, V for every row, Q for the CLS rows
             if fold:
+                s1, p1 = ln_stats(h2, st, pl)
                 if not last:
-                    _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, pl, L["cqkv"], LNE, q2,
-                         P, eps)
+                    _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, s1, L["cqkv"], LNE, q2,
+                         p1, eps)
                 else:
-                    _run(T, "gemm_kv", vpf.gemm, h2, L["wqkv"][D:], L["bqkv"][D:], None, None, 0, pl, L["cqkv"][D:],
-                         LNE, kv2, P, eps)
+                    _run(T, "gemm_kv", vpf.gemm, h2, L["wqkv"][D:], L["bqkv"][D:], None, None, 0, s1, L["cqkv"][D:],
+                         LNE, kv2, p1, eps)
                     _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # the CLS rows' {mean, rstd}
                     _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc,
                          L["cqkv"][:D], LNE, qc)
@@ -237,16 +255,15 @@ class ViTEngine:
                     _run(T, "gemm_q_cls", vpf.gemm, xc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, None, None,
                          BIAS, qc)
             _run(T, "attention_cls" if last else "attention", vpf.attention, qkv, A.heads, 1 if last else N, self.x[:n])
-            hh, xx, hd_, pp = (hc, xc, hidc, plc) if last else (h2, x2, hid, pl)
+            hh, xx, hd_, ss, pp = (hc, xc, hidc, stc, plc) if last else (h2, x2, hid, st, pl)
             tag = "_cls" if last else ""
             if fold:
-                _run(T, "gemm_proj" + tag, vpf.gemm_stats_, xx, L["wproj"], L["bproj"], hh, None, 0, RES, hh, pp)
-                _run(T, "gemm_fc1" + tag, vpf.gemm, hh, L["wfc1"], L["bfc1"], None, None, 0, pp, L["cfc1"], LNG, hd_,
-                     P, eps)
-                if not last:
-                    _run(T, "gemm_fc2" + tag, vpf.gemm_stats_, hd_, L["wfc2"], L["bfc2"], hh, None, 0, RES, hh, pl)
-                else:   # the last block's output only feeds the final LayerNorm (cls_weight computes its stats)
-                    _run(T, "gemm_fc2" + tag, vpf.gemm, hd_, L["wfc2"], L["bfc2"], hh, None, 0, None, None, RES, hh)
+                residual_gemm("gemm_proj" + tag, xx, L["wproj"], L["bproj"], hh, pp)
+                s2, p2 = ln_stats(hh, ss, pp)
+                _run(T, "gemm_fc1" + tag, vpf.gemm, hh, L["wfc1"], L["bfc1"], None, None, 0, s2, L["cfc1"], LNG, hd_,
+                     p2, eps)
+                # the last block's output only feeds the final LayerNorm (cls_weight computes its own stats)
+                residual_gemm("gemm_fc2" + tag, hd_, L["wfc2"], L["bfc2"], hh, None if last else pl)
             else:
                 _run(T, "gemm_proj" + tag, vpf.gemm, xx, L["wproj"], L["bproj"], hh, None, 0, None, None, RES, hh)
                 _run(T, "layernorm", vpf.layernorm, hh, L["n2g"], L["n2b"], A.ln_eps, xx)
