@@ -39,7 +39,7 @@ def name_gemms(rows, min_grid):
     for _, kname, grid, val in rows:
         if "k_gemm_bf16<" not in kname or grid < min_grid:
             continue
-        epi = kname.split("k_gemm_bf16<")[1].split(">")[0]
+        epi = kname.split("k_gemm_bf16<")[1].split(">")[0].split(",")[0].strip()
         if epi == "4":
             n = "gemm_qkv"
         elif epi == "5":
