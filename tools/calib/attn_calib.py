@@ -5,7 +5,7 @@ import torch
 sys.path.insert(0, ".")
 from vitparticlefiltertracker_amd import ops
 
-B, N, H = 4096, 197, 12
+B, N, H = int(os.environ.get("ATT_B", 4096)), 197, int(os.environ.get("ATT_H", 12))
 MODES = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1"]
 D = 64 * H
 torch.manual_seed(0)

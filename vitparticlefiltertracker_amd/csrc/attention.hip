@@ -256,11 +256,16 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 
 // Key-pipelined variant: one 512-thread workgroup per (particle, head) as above, but the K/V images land in
 // 32-key chunks and compute follows them: every wave issues its Q loads, then exactly one DMA piece per
-// chunk (waves 0-3: the chunk's four 8-row K pieces, waves 4-7: its four V pieces), in chunk order. Key tile
-// c is computed after a counted vmcnt (this wave's pieces of chunks <= c landed; later chunks stay in
+// chunk (waves 0-3: the chunk's four 8-row K pieces, waves 4-7: its four V pieces), in chunk order. Before
+// key tiles c .. c+CPB-1: a counted vmcnt (this wave's pieces of those chunks landed; later chunks stay in
 // flight) and one s_barrier (everyone's did), so the QK^T / softmax / PV of the first tiles overlap the
 // HBM fetch of the later ones instead of waiting for the whole 57 KiB image. Waves without a query strip
 // (8 waves, 7 strips at N = 197) only move data and keep the barrier count. N <= 256 (one strip per wave).
+// CPB: 32-key chunks per counted wait + barrier. Waiting for 4 chunks at a time (2 barriers at N = 197)
+// measured 3-4 % faster than per-chunk barriers (1, 2, 3, 4: 1.223 / 1.210 / 1.196 / 1.178 ms at 4096 x 12
+// heads, profiles/r1_gemm_lab/attn_cpb.txt): each barrier puts all 8 waves back in lockstep.
+constexpr int PIPE_CPB = 4;
+template <int CPB>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_pipe(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -307,15 +312,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int nfull = N >> 5;             // chunks without padded keys
     int c = 0;
     for (; c < nfull; ++c) {
-        wait_vmcnt(NT - 1 - c);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        if (c % CPB == 0) {   // chunks c .. c+CPB-1 landed for every wave
+            wait_vmcnt(max(NT - c - CPB, 0));
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        }
         if (active) attn_step<1, false, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
     }
     if (c < NT) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        if (c % CPB == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        }
         if (active) attn_step<1, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
     }
     if (!active) return;
@@ -537,12 +546,12 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     if (N <= 256 && !(mode && mode[0] == '0')) {
         static bool pipe_attr = false;   // benign race: idempotent attribute set
         if (!pipe_attr) {
-            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024);
+            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             pipe_attr = true;
         }
-        hipLaunchKernelGGL(k_attn_bf16_pipe, dim3((unsigned)(B * H)), dim3(512), lds, (hipStream_t)stream, qkv, out,
-                           N, H, scale_log2, q_rows);
+        hipLaunchKernelGGL(k_attn_bf16_pipe<PIPE_CPB>, dim3((unsigned)(B * H)), dim3(512), lds, (hipStream_t)stream,
+                           qkv, out, N, H, scale_log2, q_rows);
         VPF_RETURN_LAUNCH();
     }
     const int threads = 64 * (strips < 8 ? strips : 8);
