@@ -249,7 +249,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     // Grouped order inside each XCD's contiguous lid range: groups of `group` A row-panels; within a group
     // the A panel index runs fastest, so the ~32 tiles an XCD has in flight cover ~group A panels x
     // 32/group W panels and both stay in that XCD's L2 (tm-major order re-fetched a 393 KB W panel per
-    // tile on FC1: FETCH_SIZE 14.8 GB/launch, profiles/r1_notes.md). group = 0: plain tm-major.
+    // tile on FC1: FETCH_SIZE 14.8 GB/launch, profiles/r1_notes.md). group = 0: plain tm-major. Default 4
+    // (4 A x 8 W panels in flight per XCD: ~11-12 distinct K-slices per K-step for 32 tiles, the minimum of
+    // a + b at a*b = 32): sweep 2..24 in profiles/r1_gemm_lab/group_sweep.txt, 4 best or tied on all shapes.
     const int tiles_n = (N + BN - 1) / BN;
     int tm, tn;
     if (group > 0) {
@@ -438,7 +440,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
 
 static int g_group = -1;
 static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size of the tile order (0 = tm-major)
-    if (g_group < 0) { const char* e = getenv("VPF_GEMM_GROUP"); g_group = e ? atoi(e) : 8; if (g_group < 0) g_group = 0; }
+    if (g_group < 0) { const char* e = getenv("VPF_GEMM_GROUP"); g_group = e ? atoi(e) : 4; if (g_group < 0) g_group = 0; }
     return g_group;
 }
 
