@@ -18,7 +18,7 @@ import threading
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvpf.so")
+LIB_PATH = os.environ.get("VPF_LIB_PATH") or os.path.join(_HERE, "libvpf.so")   # override: A/B tooling only
 CSRC = os.path.join(_HERE, "csrc")
 
 _lock = threading.Lock()

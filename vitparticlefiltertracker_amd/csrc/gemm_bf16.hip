@@ -371,27 +371,33 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             la = smem + (kt % 3) * OPERAND_BYTES;
             lb = smem + (3 + (kt & 1)) * OPERAND_BYTES;
         }
+        // both 32-deep halves' fragments are read up front (24 ds_read_b128): the second half's reads
+        // complete under the first half's 32 MFMAs instead of stalling between them
+        bf16x8 a[2][8], b[2][4];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            bf16x8 a[8], b[4];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int row = wm * 128 + i * 16 + fr;
-                const int ch = (ks * 4 + fq) ^ ((row >> 1) & 7);
-                a[i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + ch * 16);
-            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int row = wn * 64 + j * 16 + fr;
                 const int ch = (ks * 4 + fq) ^ ((row >> 1) & 7);
-                b[j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + ch * 16);
+                b[ks][j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + ch * 16);
             }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = wm * 128 + i * 16 + fr;
+                const int ch = (ks * 4 + fq) ^ ((row >> 1) & 7);
+                a[ks][i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + ch * 16);
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
-                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[j][i], 0, 0, 0);
-        }
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], a[ks][i], acc[j][i], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads first
+        __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);   // then the 64 MFMAs (counted lgkmcnt waits)
     }
 
     // ---------------- epilogue ----------------
