@@ -36,9 +36,7 @@ constexpr int OPERAND_BYTES = BM * BK * 2;      // 32 KiB per operand tile
 constexpr int STAGE_BYTES = 2 * OPERAND_BYTES;  // A + B
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KiB
 // epilogue operands: bias (1 KiB) | colsum (1 KiB) | row statistics (up to MAX_PARTS planes of 2 KiB)
-// (consumers) or the producers' per-wave row partials (8 x 128 rows x 8 B) at 2 KiB
 constexpr int MAX_PARTS = 15;
-constexpr int AUX_RED = 2048;
 constexpr int AUX_BYTES = 2048 + MAX_PARTS * 2048;
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
@@ -60,13 +58,6 @@ __device__ __forceinline__ f32x2 gelu_sig2(f32x2 x) {
     return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
-// Sum of a float over the 8 consecutive lanes of each lane octet (DPP: quad swaps, then half-row mirror).
-__device__ __forceinline__ float octet_sum(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
-    return v;
-}
 
 // Epilogue of one wave's 128 (M) x 64 (N) sub-tile. `img` is this wave's private 16 KiB of LDS (free of any
 // operand the other waves still read), `aux` the epilogue-operand region (bias | colsum at column offset
@@ -74,13 +65,14 @@ __device__ __forceinline__ float octet_sum(float v) {
 // accumulators, bf16 pack, 8-B writes into an XOR-swizzled image, then 16-B coalesced row stores (+ residual
 // / position-embedding adds on the packed values). `stats_out` (may be null): for the producers of the
 // residual stream (EPI_BIAS_RESIDUAL, EPI_PATCH) the per-row {sum, sumsq} of the stored bf16 values over the
-// wave's 64 columns go to plane n0/64 + wn (plane stride stats_rows rows), staged through the wave's 1 KiB
-// of `red` (LDS) so that each lane stores two rows with one 16-B store; no cross-wave step.
+// wave's 64 columns go to plane n0/64 + wn (plane stride stats_rows rows): each lane's 8-value partial is
+// parked in the image row it was just read from, then each lane sums the 8 partials of two rows and stores
+// them with one 16-B store; no cross-wave step.
 template <int EPI>
 __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
                                                 int m0, int n0, int lane, const bf16_t* residual,
                                                 const float* __restrict__ pos, int g2, bf16_t* C, int ldc, int M,
-                                                int N, float2* red, float* stats_out, int stats_rows) {
+                                                int N, float* stats_out, int stats_rows) {
     constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
     const int fr = lane & 15, fq = lane >> 4;
     float4 bv[4], cv[4];
@@ -174,8 +166,8 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
             v = make_uint4(o[0], o[1], o[2], o[3]);
         }
         if constexpr (PROD) {
-            if (red != nullptr) {   // wave-uniform
-                // {sum, sumsq} of the 8 stored values, then over the row's 8 lanes (64 columns)
+            if (stats_out != nullptr) {   // wave-uniform
+                // {sum, sumsq} of the lane's 8 stored values
                 // v_dot2_f32_bf16 on the packed pairs: sum = dot(w, (1, 1)), sumsq = dot(w, w) (bf16 products are
                 // exact in fp32)
                 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
@@ -189,18 +181,26 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
                     s2 = __builtin_amdgcn_fdot2_f32_bf16(pr, pr, s2, false);
                 }
                 if (!ok) { s1 = 0.f; s2 = 0.f; }
-                s1 = octet_sum(s1);
-                s2 = octet_sum(s2);
-                if (c16 == 0) red[row] = make_float2(s1, s2);
+                // the lane's partial goes back into the image row it was just read from (8 B at c16 * 8; the
+                // whole row was read by this same instruction above and LDS ops of one wave stay in order)
+                *reinterpret_cast<float2*>(img + row * 128 + c16 * 8) = make_float2(s1, s2);
             }
         }
         if (ok) *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
     }
     if constexpr (PROD) {
         const int nb = n0 + wn * 64;
-        if (red != nullptr && nb < N) {   // wave-uniform
+        if (stats_out != nullptr && nb < N) {   // wave-uniform
             __builtin_amdgcn_wave_barrier();
-            const float4 t = *reinterpret_cast<const float4*>(red + 2 * lane);   // rows 2*lane, 2*lane+1
+            // rows 2*lane, 2*lane+1: the 8 lane partials of each (64 B at the row start)
+            float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 u0 = *reinterpret_cast<const float4*>(img + (2 * lane) * 128 + q * 16);
+                const float4 u1 = *reinterpret_cast<const float4*>(img + (2 * lane + 1) * 128 + q * 16);
+                t.x += u0.x + u0.z; t.y += u0.y + u0.w;
+                t.z += u1.x + u1.z; t.w += u1.y + u1.w;
+            }
             float* plane = stats_out + (int64_t)(nb >> 6) * stats_rows * 2;
             const int m = m0 + wm * 128 + 2 * lane;
             if constexpr (EPI == VPF_EPI_PATCH) {
@@ -236,8 +236,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     // operands go into the A slot no K-tile uses any more (slot nk % 3, DMA'd at K-tile max(nk-2, 0)).
     // !DEEP: the 2-stage A+B ring (2 x 64 KiB + 4 KiB aux), kept for A/B timing (vpf_gemm_tune).
     constexpr int SMEM = DEEP ? 5 * OPERAND_BYTES : LDS_BYTES + AUX_BYTES;
-    static_assert(AUX_BYTES <= OPERAND_BYTES && AUX_RED + 8 * 1024 <= AUX_BYTES,
-                  "aux region must fit the free A slot of the deep ring");
+    static_assert(AUX_BYTES <= OPERAND_BYTES, "aux region must fit the free A slot of the deep ring");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -333,13 +332,24 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             if (wid == 1)
                 __builtin_amdgcn_global_load_lds((gptr_t)(colsum + min(n0 + lane * 4, N - 4)), (lptr_t)(aux + 1024), 16,
                                                  0, 0);
-            // stats_parts == 0: one {mean, rstd} plane; else stats_parts {sum, sumsq} planes of M rows each
+            // stats_parts == 0: one {mean, rstd} plane; else stats_parts {sum, sumsq} planes of M rows each.
+            // A plane's 256-row slice is 2 KiB = two 16-B-per-lane pieces (M even, 16-B aligned base),
+            // dealt round-robin over the 8 waves (12 planes: 3 pieces per wave instead of 12 4-B pieces).
             const float* sd = reinterpret_cast<const float*>(stats);
             const int planes = stats_parts > 0 ? stats_parts : 1;
-            for (int p = 0; p < planes; ++p)
-                __builtin_amdgcn_global_load_lds(
-                    (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + wid * 64 + lane, 2 * M - 1)),
-                    (lptr_t)(aux + 2048 + p * 2048 + wid * 256), 4, 0, 0);
+            if ((M & 1) == 0 && ((uintptr_t)sd & 15) == 0) {
+                for (int pc = wid; pc < 2 * planes; pc += 8) {
+                    const int p = pc >> 1, hf = pc & 1;
+                    __builtin_amdgcn_global_load_lds(
+                        (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + hf * 256 + lane * 4, 2 * M - 4)),
+                        (lptr_t)(aux + 2048 + p * 2048 + hf * 1024), 16, 0, 0);
+                }
+            } else {
+                for (int p = 0; p < planes; ++p)
+                    __builtin_amdgcn_global_load_lds(
+                        (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + wid * 64 + lane, 2 * M - 1)),
+                        (lptr_t)(aux + 2048 + p * 2048 + wid * 256), 4, 0, 0);
+            }
         }
     };
     if constexpr (!DEEP) {
@@ -424,9 +434,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         const int region = (wid >> 1) + ((wid >> 1) >= (nk % 3) ? 1 : 0);
         img = smem + region * OPERAND_BYTES + (wid & 1) * 16384;
     }
-    float2* red = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) && stats_out != nullptr
-                      ? reinterpret_cast<float2*>(aux + AUX_RED) + wid * 128 : nullptr;
-    store_wave_tile<EPI>(img, aux, acc, wm, wn, m0, n0, lane, residual, pos, g2, C, ldc, M, N, red, stats_out,
+    float* prod_stats = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) ? stats_out : nullptr;
+    store_wave_tile<EPI>(img, aux, acc, wm, wn, m0, n0, lane, residual, pos, g2, C, ldc, M, N, prod_stats,
                          stats_rows);
 }
 
