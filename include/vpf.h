@@ -70,8 +70,9 @@ int vpf_cls_rows_f32(float* tokens, int64_t n_part, int N, int D, const float* c
  * g2 = patch_rows, M % g2 == 0); EPI_LN / EPI_LN_GELU (LayerNorm folded into the GEMM, A = the raw
  * residual stream): W = W * diag(gamma), colsum fp32[N] = sum_k W[n][k] (of the bf16 W), bias = b + W_orig beta,
  * and row_stats either (stats_parts == 0) fp32[M][2] = {mean, rstd} of A's rows (vpf_row_stats_*), or
- * (stats_parts = P in 1..15) fp32[P][M][2] planes of {sum, sumsq} over disjoint column blocks of A's rows (the
- * stats_out of the GEMM that produced A), combined with eps = ln_eps: rstd = 1/sqrt(sumsq/K - mean^2 + eps).
+ * (stats_parts = P in 1..16; 1..15 under vpf_gemm_tune kernel 2) fp32[P][M][2] planes of {sum, sumsq} over
+ * disjoint column blocks of A's rows (the stats_out of the GEMM that produced A), combined with eps = ln_eps:
+ * rstd = 1/sqrt(sumsq/K - mean^2 + eps).
  * stats_out (EPI_BIAS_RESIDUAL / EPI_PATCH only, may be NULL): fp32[ceil(N/64)][R][2] planes, plane t =
  * {sum, sumsq} of the stored bf16 values of each output row over columns [64t, 64t+64); R = M, or
  * (M/g2)*(g2+1) token rows for EPI_PATCH (plane rows of the CLS tokens are left to vpf_cls_rows_bf16).

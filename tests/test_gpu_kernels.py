@@ -202,11 +202,12 @@ def _planes_ref(y: torch.Tensor, P: int) -> torch.Tensor:
     return torch.stack(out)
 
 
-@pytest.mark.parametrize("M,D", [(777, 768), (300, 192), (513, 960)])
+@pytest.mark.parametrize("M,D", [(777, 768), (300, 192), (513, 960), (512, 1024), (777, 1024)])
 def test_gemm_stats_planes(M, D):
     """Residual-stream statistics planes (bf16 LN fold without a row_stats pass): the EPI_BIAS_RESIDUAL producer
     writes {sum, sumsq} of its stored bf16 rows per 256-column block; an EPI_LN consumer reading those planes
-    (stats_parts = P, ln_eps) equals LayerNorm -> GEMM on the same rows."""
+    (stats_parts = P, ln_eps) equals LayerNorm -> GEMM on the same rows. D = 1024 (16 planes, ViT-L) takes the
+    consumer's wide path (planes land in a free operand slot at the last K-step)."""
     torch.manual_seed(M + D)
     P = (D + 63) // 64
     x = (torch.randn(M, D, device=DEV) * 0.7).to(torch.bfloat16)

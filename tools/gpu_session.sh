@@ -23,6 +23,9 @@ for step in "$@"; do
     bench)
       timeout -k 10 900 python bench.py --steps 5 --warmup 2 > $OUT/bench.log 2>&1
       ok_or_stop $? bench; tail -3 $OUT/bench.log ;;
+    bench_l)
+      timeout -k 10 900 python bench.py --arch vit_large_patch14_336 --steps 2 --warmup 1 --cpu-seconds 0 > $OUT/bench_l.log 2>&1
+      ok_or_stop $? bench_l; tail -1 $OUT/bench_l.log | cut -c1-400 ;;
     bench_np)
       VPF_GEMM_PERSISTENT=0 timeout -k 10 900 python bench.py --steps 5 --warmup 2 --cpu-seconds 0 > $OUT/bench_np.log 2>&1
       ok_or_stop $? bench_np; tail -1 $OUT/bench_np.log | cut -c1-400 ;;

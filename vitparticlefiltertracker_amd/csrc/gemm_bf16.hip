@@ -35,9 +35,12 @@ constexpr int NTHREADS = 512;
 constexpr int OPERAND_BYTES = BM * BK * 2;      // 32 KiB per operand tile
 constexpr int STAGE_BYTES = 2 * OPERAND_BYTES;  // A + B
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KiB
-// epilogue operands: bias (1 KiB) | colsum (1 KiB) | row statistics (up to MAX_PARTS planes of 2 KiB)
-constexpr int MAX_PARTS = 15;
-constexpr int AUX_BYTES = 2048 + MAX_PARTS * 2048;
+// epilogue operands: bias (1 KiB) | colsum (1 KiB) | row statistics (up to AUX_PARTS planes of 2 KiB).
+// 16 planes (D = 1024) do not fit next to bias / colsum: the deep ring then lands them in a second free A
+// slot at the last K-step (wide path).
+constexpr int AUX_PARTS = 15;
+constexpr int MAX_PARTS = 16;
+constexpr int AUX_BYTES = 2048 + AUX_PARTS * 2048;
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -220,7 +223,7 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
     }
 }
 
-template <int EPI, bool DEEP>
+template <int EPI, bool DEEP, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W,
                                                         const float* __restrict__ bias,
@@ -325,6 +328,29 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
     const int nk = K / BK;
     char* aux = DEEP ? smem + (nk % 3) * OPERAND_BYTES : smem + LDS_BYTES;
+    // stats_parts == 0: one {mean, rstd} plane; else stats_parts {sum, sumsq} planes of M rows each. A
+    // plane's 256-row slice is 2 KiB = two 16-B-per-lane pieces (M even, 16-B aligned base), dealt round-robin
+    // over the 8 waves (12 planes: 3 pieces per wave instead of 12 4-B pieces).
+    constexpr bool LN_ = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    constexpr bool wide = DEEP && LN_ && WIDE;   // host: only for stats_parts > AUX_PARTS
+    char* planes_lds = wide ? smem + ((nk + 1) % 3) * OPERAND_BYTES : aux + 2048;
+    auto load_planes = [&](char* dst) {
+        const float* sd = reinterpret_cast<const float*>(stats);
+        const int planes = stats_parts > 0 ? stats_parts : 1;
+        if ((M & 1) == 0 && ((uintptr_t)sd & 15) == 0) {
+            for (int pc = wid; pc < 2 * planes; pc += 8) {
+                const int p = pc >> 1, hf = pc & 1;
+                __builtin_amdgcn_global_load_lds(
+                    (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + hf * 256 + lane * 4, 2 * M - 4)),
+                    (lptr_t)(dst + p * 2048 + hf * 1024), 16, 0, 0);
+            }
+        } else {
+            for (int p = 0; p < planes; ++p)
+                __builtin_amdgcn_global_load_lds(
+                    (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + wid * 64 + lane, 2 * M - 1)),
+                    (lptr_t)(dst + p * 2048 + wid * 256), 4, 0, 0);
+        }
+    };
     auto load_aux = [&]() {
         if (wid == 0)
             __builtin_amdgcn_global_load_lds((gptr_t)(bias + min(n0 + lane * 4, N - 4)), (lptr_t)aux, 16, 0, 0);
@@ -332,24 +358,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             if (wid == 1)
                 __builtin_amdgcn_global_load_lds((gptr_t)(colsum + min(n0 + lane * 4, N - 4)), (lptr_t)(aux + 1024), 16,
                                                  0, 0);
-            // stats_parts == 0: one {mean, rstd} plane; else stats_parts {sum, sumsq} planes of M rows each.
-            // A plane's 256-row slice is 2 KiB = two 16-B-per-lane pieces (M even, 16-B aligned base),
-            // dealt round-robin over the 8 waves (12 planes: 3 pieces per wave instead of 12 4-B pieces).
-            const float* sd = reinterpret_cast<const float*>(stats);
-            const int planes = stats_parts > 0 ? stats_parts : 1;
-            if ((M & 1) == 0 && ((uintptr_t)sd & 15) == 0) {
-                for (int pc = wid; pc < 2 * planes; pc += 8) {
-                    const int p = pc >> 1, hf = pc & 1;
-                    __builtin_amdgcn_global_load_lds(
-                        (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + hf * 256 + lane * 4, 2 * M - 4)),
-                        (lptr_t)(aux + 2048 + p * 2048 + hf * 1024), 16, 0, 0);
-                }
-            } else {
-                for (int p = 0; p < planes; ++p)
-                    __builtin_amdgcn_global_load_lds(
-                        (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + wid * 64 + lane, 2 * M - 1)),
-                        (lptr_t)(aux + 2048 + p * 2048 + wid * 256), 4, 0, 0);
-            }
+            if (!wide) load_planes(aux + 2048);
         }
     };
     if constexpr (!DEEP) {
@@ -378,6 +387,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             if (kt + 1 < nk) stage_b(kt + 1);
             if (kt + 2 < nk) stage_a(kt + 2);
             if (kt == (nk >= 2 ? nk - 2 : 0)) load_aux();
+            if (wide && kt == nk - 1) load_planes(planes_lds);   // slot of A(nk-2): free after this barrier
             la = smem + (kt % 3) * OPERAND_BYTES;
             lb = smem + (3 + (kt & 1)) * OPERAND_BYTES;
         }
@@ -415,10 +425,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         // statistics planes -> {mean, rstd} once per row (in place over plane 0, which only this thread
         // reads), instead of in each of the 4 waves that share the row; the aux DMA landed before the last
         // K-step's barrier
+        if constexpr (wide) {   // the planes DMA'd at the last K-step must land for every wave
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
         if (stats_parts > 0 && tid < BM) {
             float sm = 0.f, sq = 0.f;
             for (int p = 0; p < stats_parts; ++p) {
-                const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + p * 2048 + tid * 8);
+                const float2 st = *reinterpret_cast<const float2*>(planes_lds + p * 2048 + tid * 8);
                 sm += st.x;
                 sq += st.y;
             }
@@ -441,12 +456,17 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
 
 }  // namespace
 
+#define VPF_IS_LN(E) ((E) == VPF_EPI_LN || (E) == VPF_EPI_LN_GELU)
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
         if (kern == 2)                                                                                       \
             hipLaunchKernelGGL((k_gemm_bf16<E, false>), grid, block, 0, s, A, (int)lda, W, bias, residual, pos, \
                                patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, \
                                k, group, stats_parts, ln_eps, stats_out, stats_rows);                        \
+        else if (VPF_IS_LN(E) && stats_parts > AUX_PARTS)                                                    \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, VPF_IS_LN(E)>), grid, block, 0, s, A, (int)lda, W,        \
+                               bias, residual, pos, patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, \
+                               C, (int)ldc, m, n, k, group, stats_parts, ln_eps, stats_out, stats_rows);     \
         else                                                                                                 \
             hipLaunchKernelGGL((k_gemm_bf16<E, true>), grid, block, 0, s, A, (int)lda, W, bias, residual, pos,  \
                                patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, \
@@ -489,7 +509,8 @@ VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, con
     if ((epilogue == VPF_EPI_LN || epilogue == VPF_EPI_LN_GELU) && (!row_stats || !colsum)) return VPF_ERR_ARG;
     // bias / colsum are DMA'd in 16-B pieces, row stats in 4-B pieces
     if (((uintptr_t)bias & 15) || ((uintptr_t)colsum & 15) || ((uintptr_t)row_stats & 7)) return VPF_ERR_ARG;
-    if (stats_parts < 0 || stats_parts > MAX_PARTS || !(ln_eps >= 0.f)) return VPF_ERR_ARG;
+    if (stats_parts < 0 || stats_parts > (gemm_kernel() == 2 ? AUX_PARTS : MAX_PARTS) || !(ln_eps >= 0.f))
+        return VPF_ERR_ARG;
     if (stats_out && (((uintptr_t)stats_out & 7) || (epilogue != VPF_EPI_BIAS_RESIDUAL && epilogue != VPF_EPI_PATCH)))
         return VPF_ERR_ARG;
     // producer plane stride: rows of C (EPI_PATCH interleaves one CLS row per patch_rows rows)

@@ -153,9 +153,9 @@ class ViTEngine:
         self.stats = torch.empty(n * N, 2, device=dev, dtype=torch.float32)
         # bf16 fold mode: residual-stream statistics planes written by the GEMMs that produce h (patch embed,
         # proj, fc2) and read by the LN-folded GEMMs (qkv, fc1): [P][rows][2] {sum, sumsq} per 64-column block.
-        # P <= 15 (the consumer's LDS copy); wider models (ViT-L, D = 1024) keep the row_stats pass.
+        # P <= 16 (the consumer's LDS copy, ViT-L's D = 1024); wider models keep the row_stats pass.
         self.parts = (D + 63) // 64
-        self.use_planes = self.fold_ln and self.parts <= 15
+        self.use_planes = self.fold_ln and self.parts <= 16
         self.planes_flat = torch.empty(self.parts * n * N * 2, device=dev, dtype=torch.float32)
         self.planes_cls_flat = torch.empty(self.parts * n * 2, device=dev, dtype=torch.float32)
         self.Q = torch.empty(n, device=dev, dtype=torch.int64)
