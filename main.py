@@ -6,6 +6,7 @@ Multi-GPU: `torchrun --nproc-per-node G --master-addr 127.0.0.1 main.py` shards 
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -22,7 +23,7 @@ def main(argv=None) -> int:
     import torch
     import torch.distributed as dist
     from vitparticlefiltertracker_amd import Tracker, load_config
-    from vitparticlefiltertracker_amd.frames import iter_frames, synthetic_clip
+    from vitparticlefiltertracker_amd.frames import iter_frames, prefetch, synthetic_clip
 
     cfg = load_config(args.config)
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
@@ -31,14 +32,15 @@ def main(argv=None) -> int:
     inp = cfg["input"]
     n = args.frames or int(inp["frames"])
     if inp["source"] == "synthetic":
-        frames = synthetic_clip(n, inp["height"], inp["width"], tuple(inp["bbox0"]), inp["seed"])
+        src = iter_frames(synthetic_clip(n, inp["height"], inp["width"], tuple(inp["bbox0"]), inp["seed"]))
     else:
-        frames = list(iter_frames(inp["source"]))[:n]
+        src = itertools.islice(iter_frames(inp["source"]), n)
+    frames = prefetch(src, depth=2)   # decode + pin on a host thread, overlapped with the GPU frame loop
     tr = Tracker(cfg)
-    tr.init(frames[0], inp["bbox0"])
+    tr.init(next(frames), inp["bbox0"])
     t0 = time.perf_counter()
     out = []
-    for k, f in enumerate(frames[1:], start=1):
+    for k, f in enumerate(frames, start=1):
         x, y, s = tr.track(f)
         out.append({"frame": k, "x": x, "y": y, "scale": s})
         if tr.rank == 0:

@@ -76,6 +76,14 @@ class Tracker:
                 self._graph = None
             self._frame_dev.copy_(src)
             return self._frame_dev
+        if (isinstance(frame, torch.Tensor) and frame.dtype == torch.uint8 and frame.dim() == 3
+                and frame.shape[2] == 3 and frame.is_contiguous() and frame.is_pinned()):
+            # frames.prefetch() output: already staged in pinned memory, copy straight from it
+            if self._frame_dev is None or self._frame_dev.shape != frame.shape:
+                self._frame_dev = torch.empty(frame.shape, dtype=torch.uint8, device=self.device)
+                self._graph = None
+            self._frame_dev.copy_(frame, non_blocking=True)
+            return self._frame_dev
         arr = np.ascontiguousarray(frame.cpu().numpy() if isinstance(frame, torch.Tensor) else frame, dtype=np.uint8)
         if arr.ndim != 3 or arr.shape[2] != 3:
             raise ValueError("frame must be uint8[H][W][3]")
