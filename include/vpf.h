@@ -76,16 +76,44 @@ int vpf_cls_rows_f32(float* tokens, int64_t n_part, int N, int D, const float* c
  * stats_out (EPI_BIAS_RESIDUAL / EPI_PATCH only, may be NULL): fp32[ceil(N/64)][R][2] planes, plane t =
  * {sum, sumsq} of the stored bf16 values of each output row over columns [64t, 64t+64); R = M, or
  * (M/g2)*(g2+1) token rows for EPI_PATCH (plane rows of the CLS tokens are left to vpf_cls_rows_bf16).
+ * C8 / Cs (EPI_BIAS_RESIDUAL / EPI_PATCH only, may be NULL): an MX8 copy of the stored bf16 output (rows as in
+ * C: token rows for EPI_PATCH) — the A operand of a following vpf_gemm_mx8; ld8 bytes per element row,
+ * lds_c >= output rows; requires N % 128 == 0 (see "MX8 operands" below).
  * Unused pointers may be NULL. Requires K % 64 == 0, N % 8 == 0, lda % 8 == 0, ldc % 8 == 0. */
 int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, const float* bias,
                   const uint16_t* residual, const float* pos, int patch_rows, const float* row_stats,
                   const float* colsum, uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                  int epilogue, int stats_parts, float ln_eps, float* stats_out, void* stream);
-/* Tuning knob for vpf_gemm_bf16 (process-wide; call it only between launches). kernel: 1 = one 256x256
- * tile per 512-thread workgroup, 2 = two 256x128-tile workgroups per CU (K % 32 == 0), 3..8 = measurement
- * variants (tools/gemm_ab.py). group: A-panel group size of the tile order (0 = row-major; < 0 = keep).
- * Initial values come from VPF_GEMM_KERNEL / VPF_GEMM_GROUP. Returns VPF_ERR_ARG for an unknown kernel. */
+                  int epilogue, int stats_parts, float ln_eps, float* stats_out, uint8_t* C8, int64_t ld8,
+                  uint32_t* Cs, int64_t lds_c, void* stream);
+/* Tuning knob for vpf_gemm_bf16 (process-wide; call it only between launches). kernel: 1 = the deep-ring
+ * kernel (3 A + 2 B K-tiles in LDS; the product), 2 = the 2-stage ring (A/B timing; no fp8 output, <= 15
+ * planes). group: A-panel group size of the tile order, also used by vpf_gemm_mx8 (0 = row-major; < 0 =
+ * keep). Initial values come from VPF_GEMM_KERNEL / VPF_GEMM_GROUP. Returns VPF_ERR_ARG for an unknown kernel. */
 int vpf_gemm_tune(int kernel, int group);
+
+/* MX8 operands (OCP MX-FP8: e4m3fn elements, one e8m0 scale per 32 consecutive K values):
+ *   elements X8[r][k] (uint8, row stride ld8 bytes); scales (e8m0 bytes) in one plane of lds uint32 words per
+ *   128-deep K-tile (lds % 64 == 0, lds >= rows), rows in bricks of 64: the scale of row r for K values
+ *   [32*(k/32), +32) is byte (r/16)%4 of word (k/128)*lds + (r/64)*64 + ((k/32)%4)*16 + r%16.
+ *   value(r, k) = e4m3(X8[r][k]) * 2^(scale - 127).
+ * Quantisation (vpf_quantize_mx8 and every fp8-producing epilogue): per block, E = the smallest exponent with
+ * amax * 2^-E <= 448 (no element saturates), clamped to [-127, 125]; byte = E + 127; elements = RNE(x * 2^-E).
+ *
+ * fp8 weight path (configs[4]): C[M][N] = epilogue(value(A8)[M][K] . value(W8)[N][K]^T), fp32 accumulation on
+ * v_mfma_scale_f32_16x16x128_f8f6f4. A8 / As: lda bytes per row (lda % 16 == 0), scale planes of lds_a
+ * words; W8 [N][K] bytes, Ws scale planes of N words (N % 64 == 0). Epilogues as vpf_gemm_bf16 except EPI_PATCH; LN
+ * epilogues take colsum = the row sums of value(W8) and stats_parts <= 13. C (bf16, may be NULL when C8 is
+ * given) and/or C8 / Cs (MX8 copy of the output, N % 128 == 0). 16-B aligned A8, W8, As, Ws; K % 128 == 0,
+ * N % 8 == 0. */
+int vpf_gemm_mx8(const uint8_t* A8, int64_t lda, const uint32_t* As, int64_t lds_a, const uint8_t* W8,
+                 const uint32_t* Ws, const float* bias, const uint16_t* residual, const float* row_stats,
+                 const float* colsum, uint16_t* C, int64_t ldc, uint8_t* C8, int64_t ld8, uint32_t* Cs,
+                 int64_t lds_c, int64_t M, int64_t N, int64_t K, int epilogue, int stats_parts, float ln_eps,
+                 float* stats_out, void* stream);
+/* bf16 rows -> MX8: row r of X (at X + r*ldx) -> element row r*out_stride of X8 and its scale words.
+ * K % 128 == 0, X 16-B aligned, ld8 % 8 == 0, lds >= (rows-1)*out_stride + 1. */
+int vpf_quantize_mx8(const uint16_t* X, int64_t ldx, int64_t rows, int64_t K, int64_t out_stride, uint8_t* X8,
+                     int64_t ld8, uint32_t* S, int64_t lds, void* stream);
 /* fp32 parity mode: same contract with fp32 tensors (exact-f32 MFMA, v_mfma_f32_32x32x2_f32).
  * Requires K % 32 == 0, lda % 4 == 0, ldc % 4 == 0. */
 int vpf_gemm_f32(const float* A, int64_t lda, const float* W, const float* bias, const float* residual,

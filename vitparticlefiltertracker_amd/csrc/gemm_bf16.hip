@@ -14,25 +14,23 @@
 //  * One raw s_barrier per K-step behind a counted vmcnt (the next A K-tile stays in flight across it);
 //    right after it, the DMA for B(t+1) and A(t+2) is issued and flies while the 64 MFMAs per wave run.
 //  * MFMA operands are "swapped" (W fragment as A, activation fragment as B) so the accumulator holds
-//    D[n][m]: each lane owns 4 consecutive output columns of one row. Epilogue: bias (+ GELU, gelu_sig2)
-//    in fp32 on the accumulators, bf16 pack, 8-B writes into a per-wave XOR-swizzled LDS image, then
-//    fully coalesced 16-B row stores (+ 16-B residual reads / position-embedding adds).
+//    D[n][m]: each lane owns 4 consecutive output columns of one row. Epilogue (gemm_common.h): bias
+//    (+ GELU, gelu_sig2) in fp32 on the accumulators, bf16 pack, 8-B writes into a per-wave XOR-swizzled
+//    LDS image, then fully coalesced 16-B row stores (+ 16-B residual reads / position-embedding adds), and
+//    optionally an MX-fp8 copy of the output (the A operand of the MX8 GEMMs, gemm_mx8.hip).
 //  * Workgroup -> tile mapping is XCD-aware (bijective remap, cdna_hip_programming.md §5 T1): the blocks
 //    that share an XCD walk consecutive tiles of one 256-row A panel, so the panel is an L2 hit.
 #include <stdlib.h>
-#include "vpf_common.h"
-#include "../../include/vpf.h"
+#include "gemm_common.h"
 
 using namespace vpf;
-
-typedef short bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+using namespace vpf::gemm;
 
 namespace {
 
-constexpr int BM = 256, BN = 256, BK = 64;
-constexpr int NTHREADS = 512;
+constexpr int BK = 64;
 constexpr int OPERAND_BYTES = BM * BK * 2;      // 32 KiB per operand tile
+static_assert(OPERAND_BYTES == TILE_BYTES, "bf16 K-tile geometry");
 constexpr int STAGE_BYTES = 2 * OPERAND_BYTES;  // A + B
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KiB
 // epilogue operands: bias (1 KiB) | colsum (1 KiB) | row statistics (up to AUX_PARTS planes of 2 KiB).
@@ -42,188 +40,7 @@ constexpr int AUX_PARTS = 15;
 constexpr int MAX_PARTS = 16;
 constexpr int AUX_BYTES = 2048 + AUX_PARTS * 2048;
 
-typedef const __attribute__((address_space(1))) void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// bf16-path GELU, two values at a time: x * sigmoid(x (a + b x^2)) = x / (1 + 2^(x (c1 + c2 x^2))), with (a, b)
-// the minimax fit to the exact-erf GELU over [-10, 10] (a = 1.6003142, b = 0.0694018; the tanh form's
-// a = 2 sqrt(2/pi), b = 0.044715 a has 4.7e-4): max |error| 2.7e-4, an eighth of the bf16 half-ulp at |y| = 1.
-// 9 instructions per pair (3 packed mul/fma, 2 v_exp_f32, 1 packed add, 2 v_rcp_f32, 1 packed mul) against
-// ~21 + hazard nops for gelu_erf2. x -> -inf: 2^(+inf) = inf, rcp = 0, y = -0; x -> +inf: y = x.
-__device__ __forceinline__ f32x2 gelu_sig2(f32x2 x) {
-    constexpr float L2E = 1.4426950408889634f;
-    constexpr float c1 = -1.6003141571059616f * L2E, c2 = -0.06940178687219423f * L2E;
-    const f32x2 q = (x * x) * c2 + c1;
-    const f32x2 t = x * q;
-    const f32x2 d = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.0f;
-    return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-}
-
-
-// Epilogue of one wave's 128 (M) x 64 (N) sub-tile. `img` is this wave's private 16 KiB of LDS (free of any
-// operand the other waves still read), `aux` the epilogue-operand region (bias | colsum at column offset
-// wn*64 of the tile, row statistics at row offset wm*128). Bias / LN-fold / GELU in fp32 on the
-// accumulators, bf16 pack, 8-B writes into an XOR-swizzled image, then 16-B coalesced row stores (+ residual
-// / position-embedding adds on the packed values). `stats_out` (may be null): for the producers of the
-// residual stream (EPI_BIAS_RESIDUAL, EPI_PATCH) the per-row {sum, sumsq} of the stored bf16 values over the
-// wave's 64 columns go to plane n0/64 + wn (plane stride stats_rows rows): each lane's 8-value partial is
-// parked in the image row it was just read from, then each lane sums the 8 partials of two rows and stores
-// them with one 16-B store; no cross-wave step.
-template <int EPI>
-__device__ __forceinline__ void store_wave_tile(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
-                                                int m0, int n0, int lane, const bf16_t* residual,
-                                                const float* __restrict__ pos, int g2, bf16_t* C, int ldc, int M,
-                                                int N, float* stats_out, int stats_rows) {
-    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
-    const int fr = lane & 15, fq = lane >> 4;
-    float4 bv[4], cv[4];
-    f32x2 rsx[8], rsy[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int c = (wn * 64 + j * 16 + fq * 4) * 4;
-        bv[j] = *reinterpret_cast<const float4*>(aux + c);
-        if constexpr (LN) cv[j] = *reinterpret_cast<const float4*>(aux + 1024 + c);
-    }
-    if constexpr (LN) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + (wm * 128 + i * 16 + fr) * 8);
-            rsx[i] = f32x2{st.y, st.y};                       // rstd
-            rsy[i] = f32x2{-st.y * st.x, -st.y * st.x};       // -rstd * mean
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            f32x2 v01, v23;
-            const f32x2 a01 = {acc[j][i][0], acc[j][i][1]}, a23 = {acc[j][i][2], acc[j][i][3]};
-            const f32x2 b01 = {bv[j].x, bv[j].y}, b23 = {bv[j].z, bv[j].w};
-            if constexpr (LN) {
-                // LN(x) W^T + b = rstd (x W'^T) - rstd mean colsum(W') + b'   (gamma folded into W', beta into b')
-                const f32x2 c01 = {cv[j].x, cv[j].y}, c23 = {cv[j].z, cv[j].w};
-                v01 = __builtin_elementwise_fma(rsx[i], a01, __builtin_elementwise_fma(rsy[i], c01, b01));
-                v23 = __builtin_elementwise_fma(rsx[i], a23, __builtin_elementwise_fma(rsy[i], c23, b23));
-            } else {
-                v01 = a01 + b01;
-                v23 = a23 + b23;
-            }
-            if constexpr (EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU) {
-                v01 = gelu_sig2(v01);
-                v23 = gelu_sig2(v23);
-            }
-            const int row = i * 16 + fr;              // row within the wave's 128-row image
-            const int c8 = (j * 4 + fq) ^ (row & 15);  // swizzled 8-B chunk
-            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
-                make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
-        }
-    }
-    const int c16 = lane & 7;
-    uint4 res[16];
-    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
-        // all 16 residual rows of this lane in flight at once, under the LDS round trip below
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int m = m0 + wm * 128 + it * 8 + (lane >> 3);
-            const int n = n0 + wn * 64 + c16 * 8;
-            res[it] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(residual + (int64_t)m * ldc + n)
-                                       : make_uint4(0, 0, 0, 0);
-        }
-    }
-    constexpr bool PROD = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH);
-    __builtin_amdgcn_wave_barrier();   // the image is private to this wave: LDS ops of one wave stay in order
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-        const int row = it * 8 + (lane >> 3);
-        uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
-        if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
-        const int m = m0 + wm * 128 + row;
-        const int n = n0 + wn * 64 + c16 * 8;
-        const bool ok = m < M && n < N;
-        int64_t orow = m;
-        if constexpr (EPI == VPF_EPI_PATCH) {
-            const int pi = m % g2;
-            orow = (int64_t)(m / g2) * (g2 + 1) + 1 + pi;
-            const float* pr = pos + (int64_t)(1 + pi) * N + min(n, N - 8);
-            const float4 p0 = *reinterpret_cast<const float4*>(pr);
-            const float4 p1 = *reinterpret_cast<const float4*>(pr + 4);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            const float pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-            uint32_t o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                o[e] = pack_bf2(bf2f((bf16_t)(w[e] & 0xffff)) + pv[2 * e], bf2f((bf16_t)(w[e] >> 16)) + pv[2 * e + 1]);
-            v = make_uint4(o[0], o[1], o[2], o[3]);
-        }
-        if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
-            const uint4 rv = res[it];
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
-            uint32_t o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                o[e] = pack_bf2(bf2f((bf16_t)(w[e] & 0xffff)) + bf2f((bf16_t)(rr[e] & 0xffff)),
-                                bf2f((bf16_t)(w[e] >> 16)) + bf2f((bf16_t)(rr[e] >> 16)));
-            v = make_uint4(o[0], o[1], o[2], o[3]);
-        }
-        if constexpr (PROD) {
-            if (stats_out != nullptr) {   // wave-uniform
-                // {sum, sumsq} of the lane's 8 stored values
-                // v_dot2_f32_bf16 on the packed pairs: sum = dot(w, (1, 1)), sumsq = dot(w, w) (bf16 products are
-                // exact in fp32)
-                typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-                const bf16x2_t one2 = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
-                float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, w[e]);
-                    s1 = __builtin_amdgcn_fdot2_f32_bf16(pr, one2, s1, false);
-                    s2 = __builtin_amdgcn_fdot2_f32_bf16(pr, pr, s2, false);
-                }
-                if (!ok) { s1 = 0.f; s2 = 0.f; }
-                // the lane's partial goes back into the image row it was just read from (8 B at c16 * 8; the
-                // whole row was read by this same instruction above and LDS ops of one wave stay in order)
-                *reinterpret_cast<float2*>(img + row * 128 + c16 * 8) = make_float2(s1, s2);
-            }
-        }
-        if (ok) *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
-    }
-    if constexpr (PROD) {
-        const int nb = n0 + wn * 64;
-        if (stats_out != nullptr && nb < N) {   // wave-uniform
-            __builtin_amdgcn_wave_barrier();
-            // rows 2*lane, 2*lane+1: the 8 lane partials of each (64 B at the row start)
-            float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 u0 = *reinterpret_cast<const float4*>(img + (2 * lane) * 128 + q * 16);
-                const float4 u1 = *reinterpret_cast<const float4*>(img + (2 * lane + 1) * 128 + q * 16);
-                t.x += u0.x + u0.z; t.y += u0.y + u0.w;
-                t.z += u1.x + u1.z; t.w += u1.y + u1.w;
-            }
-            float* plane = stats_out + (int64_t)(nb >> 6) * stats_rows * 2;
-            const int m = m0 + wm * 128 + 2 * lane;
-            if constexpr (EPI == VPF_EPI_PATCH) {
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int me = m + e;
-                    if (me < M) {
-                        const int64_t orow = (int64_t)(me / g2) * (g2 + 1) + 1 + me % g2;
-                        *reinterpret_cast<float2*>(plane + orow * 2) = e ? make_float2(t.z, t.w) : make_float2(t.x, t.y);
-                    }
-                }
-            } else {
-                if (m + 1 < M) *reinterpret_cast<float4*>(plane + (int64_t)m * 2) = t;
-                else if (m < M) *reinterpret_cast<float2*>(plane + (int64_t)m * 2) = make_float2(t.x, t.y);
-            }
-        }
-    }
-}
-
-template <int EPI, bool DEEP, bool WIDE = false>
+template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W,
                                                         const float* __restrict__ bias,
@@ -233,7 +50,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                                                         const float* __restrict__ colsum,
                                                         bf16_t* C, int ldc, int M, int N, int K, int group,
                                                         int stats_parts, float ln_eps, float* stats_out,
-                                                        int stats_rows) {
+                                                        int stats_rows, Out8 o8) {
     // DEEP: A ring of 3 K-tiles (A prefetched 2 K-tiles ahead: the activation panel is the operand that
     // misses L2), B ring of 2 (weights stay L2-hot); 5 x 32 KiB = all 160 KiB of LDS, and the epilogue
     // operands go into the A slot no K-tile uses any more (slot nk % 3, DMA'd at K-tile max(nk-2, 0)).
@@ -244,31 +61,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-    // ---- XCD-aware bijective block -> tile remap ----
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    // Grouped order inside each XCD's contiguous lid range: groups of `group` A row-panels; within a group
-    // the A panel index runs fastest, so the ~32 tiles an XCD has in flight cover ~group A panels x
-    // 32/group W panels and both stay in that XCD's L2 (tm-major order re-fetched a 393 KB W panel per
-    // tile on FC1: FETCH_SIZE 14.8 GB/launch, profiles/r1_notes.md). group = 0: plain tm-major. Default 4
-    // (4 A x 8 W panels in flight per XCD: ~11-12 distinct K-slices per K-step for 32 tiles, the minimum of
-    // a + b at a*b = 32): sweep 2..24 in profiles/r1_gemm_lab/group_sweep.txt, 4 best or tied on all shapes.
-    const int tiles_n = (N + BN - 1) / BN;
-    int tm, tn;
-    if (group > 0) {
-        const int tiles_m = (M + BM - 1) / BM;
-        const int per_group = group * tiles_n;
-        const int g = lid / per_group, idx = lid - g * per_group;
-        const int gm0 = g * group;
-        const int gsz = min(group, tiles_m - gm0);
-        tn = idx / gsz;
-        tm = gm0 + (idx - tn * gsz);
-    } else {
-        tm = lid / tiles_n;
-        tn = lid - tm * tiles_n;
-    }
-    const int m0 = tm * BM, n0 = tn * BN;
+    int m0, n0;
+    tile_of(M, N, group, m0, n0);   // XCD-aware grouped tile order (gemm_common.h); default group 4
 
     // ---- per-lane DMA source offsets (bytes, relative to the block's panel base) ----
     const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * lda * 2;
@@ -331,8 +125,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     // stats_parts == 0: one {mean, rstd} plane; else stats_parts {sum, sumsq} planes of M rows each. A
     // plane's 256-row slice is 2 KiB = two 16-B-per-lane pieces (M even, 16-B aligned base), dealt round-robin
     // over the 8 waves (12 planes: 3 pieces per wave instead of 12 4-B pieces).
-    constexpr bool LN_ = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
-    constexpr bool wide = DEEP && LN_ && WIDE;   // host: only for stats_parts > AUX_PARTS
+    constexpr bool wide = DEEP && LN && WIDE;   // host: only for stats_parts > AUX_PARTS
     char* planes_lds = wide ? smem + ((nk + 1) % 3) * OPERAND_BYTES : aux + 2048;
     auto load_planes = [&](char* dst) {
         const float* sd = reinterpret_cast<const float*>(stats);
@@ -450,27 +243,29 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         img = smem + region * OPERAND_BYTES + (wid & 1) * 16384;
     }
     float* prod_stats = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) ? stats_out : nullptr;
-    store_wave_tile<EPI>(img, aux, acc, wm, wn, m0, n0, lane, residual, pos, g2, C, ldc, M, N, prod_stats,
-                         stats_rows);
+    store_wave_tile<EPI, OUT8>(img, aux, acc, wm, wn, m0, n0, lane, residual, pos, g2, C, ldc, M, N, prod_stats,
+                               stats_rows, o8);
 }
 
 }  // namespace
 
 #define VPF_IS_LN(E) ((E) == VPF_EPI_LN || (E) == VPF_EPI_LN_GELU)
+#define VPF_IS_PROD(E) ((E) == VPF_EPI_BIAS_RESIDUAL || (E) == VPF_EPI_PATCH)
+#define VPF_GEMM_ARGS                                                                                        \
+    A, (int)lda, W, bias, residual, pos, patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, C,     \
+        (int)ldc, m, n, k, group, stats_parts, ln_eps, stats_out, stats_rows, o8
+// fp8 copies are produced by the residual-stream producers only (proj, patch embed): the only bf16 GEMMs
+// whose output an MX8 GEMM reads
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
         if (kern == 2)                                                                                       \
-            hipLaunchKernelGGL((k_gemm_bf16<E, false>), grid, block, 0, s, A, (int)lda, W, bias, residual, pos, \
-                               patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, \
-                               k, group, stats_parts, ln_eps, stats_out, stats_rows);                        \
+            hipLaunchKernelGGL((k_gemm_bf16<E, false>), grid, block, 0, s, VPF_GEMM_ARGS);                    \
         else if (VPF_IS_LN(E) && stats_parts > AUX_PARTS)                                                    \
-            hipLaunchKernelGGL((k_gemm_bf16<E, true, VPF_IS_LN(E)>), grid, block, 0, s, A, (int)lda, W,        \
-                               bias, residual, pos, patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, \
-                               C, (int)ldc, m, n, k, group, stats_parts, ln_eps, stats_out, stats_rows);     \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, VPF_IS_LN(E)>), grid, block, 0, s, VPF_GEMM_ARGS);       \
+        else if (VPF_IS_PROD(E) && o8.q != nullptr)                                                          \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, VPF_IS_PROD(E)>), grid, block, 0, s, VPF_GEMM_ARGS); \
         else                                                                                                 \
-            hipLaunchKernelGGL((k_gemm_bf16<E, true>), grid, block, 0, s, A, (int)lda, W, bias, residual, pos,  \
-                               patch_rows, reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, \
-                               k, group, stats_parts, ln_eps, stats_out, stats_rows);                        \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true>), grid, block, 0, s, VPF_GEMM_ARGS);                     \
     } while (0)
 
 static int g_group = -1;
@@ -486,7 +281,7 @@ static int gemm_kernel() {
     if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 2) g_kernel = 1; }
     return g_kernel;
 }
-static int tile_group();
+int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
 VPF_API int vpf_gemm_tune(int kernel, int group) {
     if (kernel < 1 || kernel > 2) return VPF_ERR_ARG;
     g_kernel = kernel;
@@ -494,10 +289,21 @@ VPF_API int vpf_gemm_tune(int kernel, int group) {
     return 0;
 }
 
+// fp8 output operand check shared with gemm_mx8.hip: element rows ld8 >= N bytes (8-B aligned pieces), scale
+// planes of lds_c >= output rows words (lds_c % 64 == 0, mx8_scale_byte), N % 128 == 0.
+int vpf_check_out8(const uint8_t* C8, int64_t ld8, const uint32_t* Cs, int64_t lds_c, int64_t rows, int64_t N) {
+    if (!C8) return Cs ? VPF_ERR_ARG : 0;
+    if (!Cs || N % 128 != 0 || ld8 < N || ld8 % 8 != 0 || ((uintptr_t)C8 & 7) || lds_c < rows || lds_c % 64 != 0 ||
+        ((uintptr_t)Cs & 3) || ld8 > INT32_MAX || lds_c > INT32_MAX / 4)
+        return VPF_ERR_ARG;
+    return 0;
+}
+
 VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, const float* bias,
                           const uint16_t* residual, const float* pos, int patch_rows, const float* row_stats,
                           const float* colsum, uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                          int epilogue, int stats_parts, float ln_eps, float* stats_out, void* stream) {
+                          int epilogue, int stats_parts, float ln_eps, float* stats_out, uint8_t* C8, int64_t ld8,
+                          uint32_t* Cs, int64_t lds_c, void* stream) {
     if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 8 != 0 || lda < K || lda % 8 != 0 || ldc < N ||
         ldc % 8 != 0)
         return VPF_ERR_ARG;
@@ -517,6 +323,11 @@ VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, con
     const int64_t srows = epilogue == VPF_EPI_PATCH ? (M / patch_rows) * (patch_rows + 1) : M;
     if (srows > INT32_MAX) return VPF_ERR_ARG;
     const int stats_rows = (int)srows;
+    // fp8 copy of C: residual-stream producers only, deep-ring kernel
+    if (C8 && ((epilogue != VPF_EPI_BIAS_RESIDUAL && epilogue != VPF_EPI_PATCH) || gemm_kernel() == 2))
+        return VPF_ERR_ARG;
+    if (vpf_check_out8(C8, ld8, Cs, lds_c, srows, N)) return VPF_ERR_ARG;
+    const Out8 o8{C8, reinterpret_cast<uint8_t*>(Cs), (int)ld8, (int)lds_c};
     const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     if (tiles > INT32_MAX) return VPF_ERR_ARG;
     hipStream_t s = (hipStream_t)stream;

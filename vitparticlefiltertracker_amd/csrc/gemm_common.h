@@ -1,0 +1,289 @@
+// Pieces shared by the bf16 GEMM (gemm_bf16.hip) and the MX-fp8 GEMM (gemm_mx8.hip): tile geometry, the
+// XCD-aware tile order, the GELU, the MX (OCP e4m3 + e8m0 block scale) quantiser, and the per-wave epilogue.
+#pragma once
+#include "vpf_common.h"
+#include "../../include/vpf.h"
+
+// host helpers defined in gemm_bf16.hip, shared with gemm_mx8.hip
+int vpf_gemm_tile_group();
+int vpf_check_out8(const uint8_t* C8, int64_t ld8, const uint32_t* Cs, int64_t lds_c, int64_t rows, int64_t N);
+
+namespace vpf {
+namespace gemm {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+constexpr int BM = 256, BN = 256;
+constexpr int NTHREADS = 512;
+constexpr int TILE_BYTES = BM * 128;       // one operand K-tile: 256 rows x 128 B (bf16 BK = 64 / fp8 BK = 128)
+
+// Workgroup -> output tile: XCD-aware bijective remap (cdna_hip_programming.md §5 T1) — consecutive blocks
+// of one XCD get consecutive logical ids — then a grouped order inside each XCD's range: groups of `group`
+// A row-panels with the A panel index running fastest, so the ~32 tiles an XCD has in flight cover ~group A
+// panels x 32/group W panels and both stay in that XCD's L2 (profiles/r1_gemm_lab/group_sweep.txt).
+// group = 0: plain tm-major.
+__device__ __forceinline__ void tile_of(int M, int N, int group, int& m0, int& n0) {
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tiles_n = (N + BN - 1) / BN;
+    int tm, tn;
+    if (group > 0) {
+        const int tiles_m = (M + BM - 1) / BM;
+        const int per_group = group * tiles_n;
+        const int g = lid / per_group, idx = lid - g * per_group;
+        const int gm0 = g * group;
+        const int gsz = min(group, tiles_m - gm0);
+        tn = idx / gsz;
+        tm = gm0 + (idx - tn * gsz);
+    } else {
+        tm = lid / tiles_n;
+        tn = lid - tm * tiles_n;
+    }
+    m0 = tm * BM;
+    n0 = tn * BN;
+}
+
+// bf16-path GELU, two values at a time: x * sigmoid(x (a + b x^2)) = x / (1 + 2^(x (c1 + c2 x^2))), with (a, b)
+// the minimax fit to the exact-erf GELU over [-10, 10] (a = 1.6003142, b = 0.0694018; the tanh form's
+// a = 2 sqrt(2/pi), b = 0.044715 a has 4.7e-4): max |error| 2.7e-4, an eighth of the bf16 half-ulp at |y| = 1.
+// 9 instructions per pair (3 packed mul/fma, 2 v_exp_f32, 1 packed add, 2 v_rcp_f32, 1 packed mul) against
+// ~21 + hazard nops for an erf polynomial. x -> -inf: 2^(+inf) = inf, rcp = 0, y = -0; x -> +inf: y = x.
+__device__ __forceinline__ f32x2 gelu_sig2(f32x2 x) {
+    constexpr float L2E = 1.4426950408889634f;
+    constexpr float c1 = -1.6003141571059616f * L2E, c2 = -0.06940178687219423f * L2E;
+    const f32x2 q = (x * x) * c2 + c1;
+    const f32x2 t = x * q;
+    const f32x2 d = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.0f;
+    return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
+// ---------------- MX fp8 (OCP e4m3fn elements, e8m0 scale per 32 consecutive K values) ----------------
+// Layout (vpf.h "MX8 operands"): elements X8[row][k] (1 B each, row stride ld8 bytes). Scales: per 128-deep
+// K-tile t a plane of lds words (lds % 64 == 0), rows in bricks of 64: the scale of (row r, K-block
+// kb = (k / 32) % 4) is byte (r / 16) % 4 of word t * lds + (r / 64) * 64 + kb * 16 + r % 16 (mx8_scale_byte).
+// A 256-row tile's scales for one K-tile are one contiguous 1 KiB DMA, and a GEMM lane (row r16 + 16 f of a
+// brick, K-block fq) finds the scales of the 4 fragments f = 0..3 it multiplies in the 4 bytes of ONE word,
+// which v_mfma_scale's op_sel picks byte by byte (no shifts, 3 scale VGPRs per K-tile instead of 12).
+__device__ __forceinline__ int64_t mx8_scale_byte(int64_t r, int k, int lds) {
+    return ((int64_t)(k >> 7) * lds + (r >> 6) * 64 + ((k >> 5) & 3) * 16 + (r & 15)) * 4 + ((r >> 4) & 3);
+}
+//
+// Block exponent: the smallest E with amax * 2^-E <= 448 (e4m3's largest finite value, 1.75 * 2^8), so no
+// element saturates; e8m0 byte = E + 127, E clamped to [-127, 125]. Elements: RNE(x * 2^-E) (x * 2^-E is exact
+// in fp32), one v_cvt_pk_fp8_f32 per pair. Dequantised value = e4m3(q) * 2^(byte - 127).
+__device__ __forceinline__ int mx8_block_exp(uint32_t amax_bf16) {   // amax as |bf16| bits (sign clear)
+    const uint32_t be = amax_bf16 >> 7;                                // biased exponent (0 = zero / subnormal)
+    const int ex = be ? (int)be - 127 : -126;
+    int E = ex - 8 + ((amax_bf16 & 0x7f) > 0x60 ? 1 : 0);             // mantissa > 1.75 needs one more
+    return min(max(E, -127), 125);
+}
+
+// 8 consecutive bf16 values of one row (one lane) -> 8 e4m3 bytes; the 32-value block is the lane's DPP quad
+// (lanes 4q .. 4q+3 hold columns 32b .. 32b+31 in order). Every lane of the quad must execute this.
+__device__ __forceinline__ uint2 mx8_quant8(uint4 v, uint32_t& e8m0) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t am = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) am = max(am, max(w[e] & 0x7fffu, (w[e] >> 16) & 0x7fffu));
+    am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0xB1, 0xF, 0xF, false));   // quad_perm(1,0,3,2)
+    am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x4E, 0xF, 0xF, false));   // quad_perm(2,3,0,1)
+    const int E = mx8_block_exp(am);
+    e8m0 = (uint32_t)(E + 127);
+    const float inv = __uint_as_float((uint32_t)(127 - E) << 23);     // 2^-E (normal for E in [-127, 125])
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)(w[0] & 0xffff)) * inv, bf2f((bf16_t)(w[0] >> 16)) * inv, 0,
+                                             false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)(w[1] & 0xffff)) * inv, bf2f((bf16_t)(w[1] >> 16)) * inv, lo,
+                                         true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)(w[2] & 0xffff)) * inv, bf2f((bf16_t)(w[2] >> 16)) * inv, 0,
+                                             false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)(w[3] & 0xffff)) * inv, bf2f((bf16_t)(w[3] >> 16)) * inv, hi,
+                                         true);
+    return make_uint2((uint32_t)lo, (uint32_t)hi);
+}
+
+// Optional MX-fp8 copy of a GEMM's bf16 output (the A operand of a following MX8 GEMM).
+struct Out8 {
+    uint8_t* q;      // elements, row stride ldq bytes (null: no fp8 output)
+    uint8_t* s;      // scale planes as bytes (mx8_scale_byte)
+    int ldq, lds;
+};
+
+// Epilogue of one wave's 128 (M) x 64 (N) sub-tile. `img` is this wave's private 16 KiB of LDS (free of any
+// operand the other waves still read), `aux` the epilogue-operand region (bias | colsum at column offset
+// wn*64 of the tile, row statistics at row offset wm*128). Bias / LN-fold / GELU in fp32 on the
+// accumulators, bf16 pack, 8-B writes into an XOR-swizzled image, then 16-B coalesced row stores (+ residual
+// / position-embedding adds on the packed values). C may be null when only the fp8 copy is wanted.
+// `stats_out` (may be null): for the producers of the residual stream (EPI_BIAS_RESIDUAL, EPI_PATCH) the
+// per-row {sum, sumsq} of the stored bf16 values over the wave's 64 columns go to plane n0/64 + wn (plane
+// stride stats_rows rows): each lane's 8-value partial is parked in the image row it was just read from,
+// then each lane sums the 8 partials of two rows and stores them with one 16-B store; no cross-wave step.
+// OUT8: the same bf16 values are also MX-quantised (mx8_quant8: a 32-column block is one DPP quad of lanes)
+// and stored as 8-B element pieces plus one scale byte per row and block.
+template <int EPI, bool OUT8>
+__device__ __forceinline__ void store_wave_tile(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
+                                                int m0, int n0, int lane, const bf16_t* residual,
+                                                const float* __restrict__ pos, int g2, bf16_t* C, int ldc, int M,
+                                                int N, float* stats_out, int stats_rows, Out8 o8) {
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    const int fr = lane & 15, fq = lane >> 4;
+    float4 bv[4], cv[4];
+    f32x2 rsx[8], rsy[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = (wn * 64 + j * 16 + fq * 4) * 4;
+        bv[j] = *reinterpret_cast<const float4*>(aux + c);
+        if constexpr (LN) cv[j] = *reinterpret_cast<const float4*>(aux + 1024 + c);
+    }
+    if constexpr (LN) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + (wm * 128 + i * 16 + fr) * 8);
+            rsx[i] = f32x2{st.y, st.y};                       // rstd
+            rsy[i] = f32x2{-st.y * st.x, -st.y * st.x};       // -rstd * mean
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            f32x2 v01, v23;
+            const f32x2 a01 = {acc[j][i][0], acc[j][i][1]}, a23 = {acc[j][i][2], acc[j][i][3]};
+            const f32x2 b01 = {bv[j].x, bv[j].y}, b23 = {bv[j].z, bv[j].w};
+            if constexpr (LN) {
+                // LN(x) W^T + b = rstd (x W'^T) - rstd mean colsum(W') + b'   (gamma folded into W', beta into b')
+                const f32x2 c01 = {cv[j].x, cv[j].y}, c23 = {cv[j].z, cv[j].w};
+                v01 = __builtin_elementwise_fma(rsx[i], a01, __builtin_elementwise_fma(rsy[i], c01, b01));
+                v23 = __builtin_elementwise_fma(rsx[i], a23, __builtin_elementwise_fma(rsy[i], c23, b23));
+            } else {
+                v01 = a01 + b01;
+                v23 = a23 + b23;
+            }
+            if constexpr (EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU) {
+                v01 = gelu_sig2(v01);
+                v23 = gelu_sig2(v23);
+            }
+            const int row = i * 16 + fr;              // row within the wave's 128-row image
+            const int c8 = (j * 4 + fq) ^ (row & 15);  // swizzled 8-B chunk
+            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
+                make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
+        }
+    }
+    const int c16 = lane & 7;
+    uint4 res[16];
+    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
+        // all 16 residual rows of this lane in flight at once, under the LDS round trip below
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int m = m0 + wm * 128 + it * 8 + (lane >> 3);
+            const int n = n0 + wn * 64 + c16 * 8;
+            res[it] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(residual + (int64_t)m * ldc + n)
+                                       : make_uint4(0, 0, 0, 0);
+        }
+    }
+    constexpr bool PROD = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH);
+    __builtin_amdgcn_wave_barrier();   // the image is private to this wave: LDS ops of one wave stay in order
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int row = it * 8 + (lane >> 3);
+        uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+        if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+        const int m = m0 + wm * 128 + row;
+        const int n = n0 + wn * 64 + c16 * 8;
+        const bool ok = m < M && n < N;
+        int64_t orow = m;
+        if constexpr (EPI == VPF_EPI_PATCH) {
+            const int pi = m % g2;
+            orow = (int64_t)(m / g2) * (g2 + 1) + 1 + pi;
+            const float* pr = pos + (int64_t)(1 + pi) * N + min(n, N - 8);
+            const float4 p0 = *reinterpret_cast<const float4*>(pr);
+            const float4 p1 = *reinterpret_cast<const float4*>(pr + 4);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const float pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = pack_bf2(bf2f((bf16_t)(w[e] & 0xffff)) + pv[2 * e], bf2f((bf16_t)(w[e] >> 16)) + pv[2 * e + 1]);
+            v = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
+            const uint4 rv = res[it];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = pack_bf2(bf2f((bf16_t)(w[e] & 0xffff)) + bf2f((bf16_t)(rr[e] & 0xffff)),
+                                bf2f((bf16_t)(w[e] >> 16)) + bf2f((bf16_t)(rr[e] >> 16)));
+            v = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        if constexpr (PROD) {
+            if (stats_out != nullptr) {   // wave-uniform
+                // {sum, sumsq} of the lane's 8 stored values
+                // v_dot2_f32_bf16 on the packed pairs: sum = dot(w, (1, 1)), sumsq = dot(w, w) (bf16 products are
+                // exact in fp32)
+                typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                const bf16x2_t one2 = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, w[e]);
+                    s1 = __builtin_amdgcn_fdot2_f32_bf16(pr, one2, s1, false);
+                    s2 = __builtin_amdgcn_fdot2_f32_bf16(pr, pr, s2, false);
+                }
+                if (!ok) { s1 = 0.f; s2 = 0.f; }
+                // the lane's partial goes back into the image row it was just read from (8 B at c16 * 8; the
+                // whole row was read by this same instruction above and LDS ops of one wave stay in order)
+                *reinterpret_cast<float2*>(img + row * 128 + c16 * 8) = make_float2(s1, s2);
+            }
+        }
+        if constexpr (OUT8) {
+            // whole quads are in or out of range together (rows: a quad is one row; columns: N % 128 == 0)
+            uint32_t e8;
+            const uint2 q = mx8_quant8(v, e8);
+            if (ok) {
+                *reinterpret_cast<uint2*>(o8.q + orow * o8.ldq + n) = q;
+                if ((c16 & 3) == 0) o8.s[mx8_scale_byte(orow, n, o8.lds)] = (uint8_t)e8;
+            }
+        }
+        if (ok && C != nullptr) *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
+    }
+    if constexpr (PROD) {
+        const int nb = n0 + wn * 64;
+        if (stats_out != nullptr && nb < N) {   // wave-uniform
+            __builtin_amdgcn_wave_barrier();
+            // rows 2*lane, 2*lane+1: the 8 lane partials of each (64 B at the row start)
+            float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 u0 = *reinterpret_cast<const float4*>(img + (2 * lane) * 128 + q * 16);
+                const float4 u1 = *reinterpret_cast<const float4*>(img + (2 * lane + 1) * 128 + q * 16);
+                t.x += u0.x + u0.z; t.y += u0.y + u0.w;
+                t.z += u1.x + u1.z; t.w += u1.y + u1.w;
+            }
+            float* plane = stats_out + (int64_t)(nb >> 6) * stats_rows * 2;
+            const int m = m0 + wm * 128 + 2 * lane;
+            if constexpr (EPI == VPF_EPI_PATCH) {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int me = m + e;
+                    if (me < M) {
+                        const int64_t orow = (int64_t)(me / g2) * (g2 + 1) + 1 + me % g2;
+                        *reinterpret_cast<float2*>(plane + orow * 2) = e ? make_float2(t.z, t.w) : make_float2(t.x, t.y);
+                    }
+                }
+            } else {
+                if (m + 1 < M) *reinterpret_cast<float4*>(plane + (int64_t)m * 2) = t;
+                else if (m < M) *reinterpret_cast<float2*>(plane + (int64_t)m * 2) = make_float2(t.x, t.y);
+            }
+        }
+    }
+}
+
+}  // namespace gemm
+}  // namespace vpf

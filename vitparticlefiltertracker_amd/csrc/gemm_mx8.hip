@@ -1,0 +1,279 @@
+// MX-fp8 GEMM for the fp8 weight path (BASELINE.json configs[4]; MI355X_MICROARCH.md
+// "Matrix cores": block-scaled e4m3 runs at twice the bf16 MFMA rate).
+//
+//   C[M][N] = epi( deq(A8)[M][K] . deq(W8)[N][K]^T ),   deq(x) = e4m3(x) * 2^(e8m0 - 127) per 32 K values,
+//
+// on v_mfma_scale_f32_16x16x128_f8f6f4 (fp32 accumulation; the hardware applies both operands' block scales).
+// Operand format (vpf.h "MX8 operands"): elements [rows][K] bytes, per 128-deep K-tile a plane of scale words
+// in 64-row bricks (gemm_common.h mx8_scale_byte). Producers: vpf_quantize_mx8 (weights, CLS
+// rows), and the epilogues of the residual-stream GEMMs (Out8) and of this kernel (FC1 -> FC2's A operand).
+//
+// Design: the bf16 kernel's geometry at twice the K per K-tile — 256x256 tile, 8 waves 2 (M) x 4 (N), each
+// wave 8 x 4 fragments of 16x16 — so a K-tile is again 256 rows x 128 B per operand with the same XOR-swizzled
+// lane-linear LDS image and 16-B DMA pieces, plus 1 KiB of scale words per operand (one 16-B piece per lane
+// of one wave). Per K-tile a wave reads 24 ds_read_b128 (two per fragment: its 32-byte K-block) and 3 scale
+// words (op_sel picks a fragment's byte), then issues 32 MFMAs (each 2x the cycles of a 16x16x32 bf16 MFMA for 4x the K). Two-stage ring
+// (2 x 66 KiB) + 28 KiB epilogue operands (bias | colsum | up to MX_PARTS statistics planes) = 160 KiB.
+// Epilogues: gemm_common.h store_wave_tile (bias / LN fold / GELU / residual, statistics planes, optional
+// MX-fp8 copy of the output).
+#include <stdlib.h>
+#include "gemm_common.h"
+
+using namespace vpf;
+using namespace vpf::gemm;
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+constexpr int BK = 128;                                // fp8 K values per K-tile (128 B per row)
+constexpr int SC_BYTES = BM * 4;                       // a K-tile's scale words for 256 rows
+constexpr int STAGE = 2 * TILE_BYTES + 2 * SC_BYTES;   // A | B | A scales | B scales
+constexpr int RING = 2 * STAGE;
+constexpr int MX_PARTS = 13;                           // statistics planes next to bias | colsum
+constexpr int AUX = 2048 + MX_PARTS * 2048;
+static_assert(RING + AUX <= 160 * 1024, "LDS budget");
+static_assert(8 * 16384 <= RING, "the 8 epilogue images live in the ring");
+
+// One W fragment (column group J of the wave) against the 8 activation fragments: op_sel (an immediate)
+// picks the scale byte — J of the W brick word, i % 4 of the activation brick words sa0 (i < 4) / sa1.
+#define VPF_MX(I, SA) \
+    acc[I] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a[I], acc[I], 0, 0, J, sb, (I) & 3, SA)
+template <int J>
+__device__ __forceinline__ void mx_col(f32x4 (&acc)[8], const i32x8& b, const i32x8 (&a)[8], int sb, int sa0, int sa1) {
+    VPF_MX(0, sa0); VPF_MX(1, sa0); VPF_MX(2, sa0); VPF_MX(3, sa0);
+    VPF_MX(4, sa1); VPF_MX(5, sa1); VPF_MX(6, sa1); VPF_MX(7, sa1);
+}
+#undef VPF_MX
+
+template <int EPI, bool OUT8>
+__global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict__ A, int lda,
+                                                       const uint32_t* __restrict__ As, int lds_a,
+                                                       const uint8_t* __restrict__ W,
+                                                       const uint32_t* __restrict__ Ws,
+                                                       const float* __restrict__ bias, const bf16_t* residual,
+                                                       const float2* __restrict__ stats,
+                                                       const float* __restrict__ colsum, bf16_t* C, int ldc,
+                                                       int M, int N, int K, int group, int stats_parts,
+                                                       float ln_eps, float* stats_out, Out8 o8) {
+    __shared__ __attribute__((aligned(16))) char smem[RING + AUX];
+    char* aux = smem + RING;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int m0, n0;
+    tile_of(M, N, group, m0, n0);
+
+    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * lda;
+    const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K;
+    uint32_t offA[4], offB[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int g = i * 8 + wid;                 // wave-instruction index: rows [8g, 8g+8)
+        const int row = 8 * g + (lane >> 3);
+        const int lch = (lane & 7) ^ ((row >> 1) & 7);
+        offA[i] = (uint32_t)min(row, M - 1 - m0) * (uint32_t)lda + (uint32_t)(lch * 16);
+        offB[i] = (uint32_t)min(row, N - 1 - n0) * (uint32_t)K + (uint32_t)(lch * 16);
+    }
+    // scale words of rows [m0 + 4 lane, +4): rows past the end read the last valid 16 B (never used)
+    const int sa_row = min(m0 + 4 * lane, lds_a - 4), sb_row = min(n0 + 4 * lane, N - 4);
+    auto stage = [&](int buf, int kt) {
+        char* st = smem + buf * STAGE;
+        const uint32_t koff = (uint32_t)kt * BK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int g = i * 8 + wid;
+            __builtin_amdgcn_global_load_lds((gptr_t)(Ablk + offA[i] + koff), (lptr_t)(st + g * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)(Bblk + offB[i] + koff), (lptr_t)(st + TILE_BYTES + g * 1024), 16,
+                                             0, 0);
+        }
+        if (wid == 0)
+            __builtin_amdgcn_global_load_lds((gptr_t)(As + (int64_t)kt * lds_a + sa_row), (lptr_t)(st + 2 * TILE_BYTES),
+                                             16, 0, 0);
+        if (wid == 1)
+            __builtin_amdgcn_global_load_lds((gptr_t)(Ws + (int64_t)kt * N + sb_row),
+                                             (lptr_t)(st + 2 * TILE_BYTES + SC_BYTES), 16, 0, 0);
+    };
+
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    auto load_aux = [&]() {
+        if (wid == 2)
+            __builtin_amdgcn_global_load_lds((gptr_t)(bias + min(n0 + lane * 4, N - 4)), (lptr_t)aux, 16, 0, 0);
+        if constexpr (LN) {
+            if (wid == 3)
+                __builtin_amdgcn_global_load_lds((gptr_t)(colsum + min(n0 + lane * 4, N - 4)), (lptr_t)(aux + 1024), 16,
+                                                 0, 0);
+            const float* sd = reinterpret_cast<const float*>(stats);
+            const int planes = stats_parts > 0 ? stats_parts : 1;
+            if ((M & 1) == 0 && ((uintptr_t)sd & 15) == 0) {
+                for (int pc = wid; pc < 2 * planes; pc += 8) {
+                    const int p = pc >> 1, hf = pc & 1;
+                    __builtin_amdgcn_global_load_lds(
+                        (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + hf * 256 + lane * 4, 2 * M - 4)),
+                        (lptr_t)(aux + 2048 + p * 2048 + hf * 1024), 16, 0, 0);
+                }
+            } else {
+                for (int p = 0; p < planes; ++p)
+                    __builtin_amdgcn_global_load_lds(
+                        (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + wid * 64 + lane, 2 * M - 1)),
+                        (lptr_t)(aux + 2048 + p * 2048 + wid * 256), 4, 0, 0);
+            }
+        }
+    };
+
+    const int wm = wid >> 2, wn = wid & 3;
+    const int fr = lane & 15, fq = lane >> 4;
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    stage(0, 0);
+    load_aux();
+    for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();   // K-tile kt landed for every wave; K-tile kt-1's buffer is free
+        if (kt + 1 < nk) stage((kt + 1) & 1, kt + 1);
+        const char* st = smem + (kt & 1) * STAGE;
+        const char* la = st;
+        const char* lb = st + TILE_BYTES;
+        const uint32_t* las = reinterpret_cast<const uint32_t*>(st + 2 * TILE_BYTES);
+        const uint32_t* lbs = las + BM;
+        // Operand map of the 16x16x128 f8 MFMA (tools/micro/mx_probe.py, profiles/r1_gemm_lab/mx_probe.txt): lane
+        // group g holds K values [16g, 16g+16) in bytes 0-15 and [64+16g, +16) in bytes 16-31 (two 16x16x64
+        // halves), and the scale of K-block b = [32b, 32b+32) comes from lane group b. So a lane reads logical
+        // chunks fq and 4+fq of its row, and supplies the scale of block fq: one word per 64-row brick, byte f
+        // = fragment f of the brick (mx8_scale_byte).
+        i32x8 a[8], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = wn * 64 + j * 16 + fr;
+            const int sw = (row >> 1) & 7;
+            const int4 lo = *reinterpret_cast<const int4*>(lb + row * 128 + (fq ^ sw) * 16);
+            const int4 hi = *reinterpret_cast<const int4*>(lb + row * 128 + ((4 + fq) ^ sw) * 16);
+            b[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = wm * 128 + i * 16 + fr;
+            const int sw = (row >> 1) & 7;
+            const int4 lo = *reinterpret_cast<const int4*>(la + row * 128 + (fq ^ sw) * 16);
+            const int4 hi = *reinterpret_cast<const int4*>(la + row * 128 + ((4 + fq) ^ sw) * 16);
+            a[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        }
+        const int sb = (int)lbs[wn * 64 + fq * 16 + fr];
+        const int sa0 = (int)las[(2 * wm) * 64 + fq * 16 + fr];
+        const int sa1 = (int)las[(2 * wm + 1) * 64 + fq * 16 + fr];
+        // swapped operands as in the bf16 kernel: W fragment as MFMA-A, activation as MFMA-B -> D[n][m]
+        mx_col<0>(acc[0], b[0], a, sb, sa0, sa1);
+        mx_col<1>(acc[1], b[1], a, sb, sa0, sa1);
+        mx_col<2>(acc[2], b[2], a, sb, sa0, sa1);
+        mx_col<3>(acc[3], b[3], a, sb, sa0, sa1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 27, 0);   // fragment + scale reads first
+        __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);   // then the 32 MFMAs
+    }
+
+    if constexpr (LN) {
+        if (stats_parts > 0 && tid < BM) {   // planes -> {mean, rstd} once per row (see gemm_bf16.hip)
+            float sm = 0.f, sq = 0.f;
+            for (int p = 0; p < stats_parts; ++p) {
+                const float2 s2 = *reinterpret_cast<const float2*>(aux + 2048 + p * 2048 + tid * 8);
+                sm += s2.x;
+                sq += s2.y;
+            }
+            const float inv_k = 1.0f / (float)K;
+            const float mean = sm * inv_k;
+            const float var = fmaxf(fmaf(sq, inv_k, -mean * mean), 0.f);
+            *reinterpret_cast<float2*>(aux + 2048 + tid * 8) = make_float2(mean, __builtin_amdgcn_rsqf(var + ln_eps));
+        }
+    }
+    __syncthreads();   // the ring is free: 8 x 16 KiB epilogue images
+    float* prod_stats = EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr;
+    store_wave_tile<EPI, OUT8>(smem + wid * 16384, aux, acc, wm, wn, m0, n0, lane, residual, nullptr, 1, C, ldc, M, N,
+                               prod_stats, M, o8);
+}
+
+// MX quantisation of bf16 rows: one lane per 8 values, a DPP quad per 32-value block (gemm_common.h).
+// Row r of X goes to row r * out_stride of X8 / the scale words (the CLS rows of a token tensor).
+__global__ __launch_bounds__(256) void k_quantize_mx8(const bf16_t* __restrict__ X, int64_t ldx, int64_t rows, int K,
+                                                      int64_t out_stride, uint8_t* __restrict__ X8, int64_t ld8,
+                                                      uint8_t* __restrict__ S, int64_t lds) {
+    const int per_row = K / 8;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = rows * per_row;
+    const int64_t tc = t < total ? t : total - 1;   // whole quads are in or out (per_row % 4 == 0)
+    const int64_t r = tc / per_row;
+    const int c = (int)(tc - r * per_row) * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(X + r * ldx + c);
+    uint32_t e8;
+    const uint2 q = mx8_quant8(v, e8);
+    if (t < total) {
+        const int64_t orow = r * out_stride;
+        *reinterpret_cast<uint2*>(X8 + orow * ld8 + c) = q;
+        if ((c & 31) == 0) S[mx8_scale_byte(orow, c, (int)lds)] = (uint8_t)e8;
+    }
+}
+
+}  // namespace
+
+#define VPF_MX8_ARGS                                                                                         \
+    A, (int)lda, As, (int)lds_a, W, Ws, bias, residual, reinterpret_cast<const float2*>(row_stats), colsum,    \
+        C, (int)ldc, (int)M, (int)N, (int)K, group, stats_parts, ln_eps, stats_out, o8
+#define VPF_MX8_LAUNCH(E)                                                                                    \
+    do {                                                                                                     \
+        if (o8.q)                                                                                            \
+            hipLaunchKernelGGL((k_gemm_mx8<E, true>), grid, block, 0, s, VPF_MX8_ARGS);                       \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_gemm_mx8<E, false>), grid, block, 0, s, VPF_MX8_ARGS);                      \
+    } while (0)
+
+VPF_API int vpf_gemm_mx8(const uint8_t* A, int64_t lda, const uint32_t* As, int64_t lds_a, const uint8_t* W,
+                         const uint32_t* Ws, const float* bias, const uint16_t* residual, const float* row_stats,
+                         const float* colsum, uint16_t* C, int64_t ldc, uint8_t* C8, int64_t ld8, uint32_t* Cs,
+                         int64_t lds_c, int64_t M, int64_t N, int64_t K, int epilogue, int stats_parts, float ln_eps,
+                         float* stats_out, void* stream) {
+    if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 8 != 0 || lda < K || lda % 16 != 0) return VPF_ERR_ARG;
+    if (M > INT32_MAX / 2 || N > 65536 || K > 65536 || lda > INT32_MAX / 2) return VPF_ERR_ARG;
+    if ((uint64_t)BM * (uint64_t)lda > UINT32_MAX) return VPF_ERR_ARG;
+    if (!A || !As || !W || !Ws || !bias || (!C && !C8)) return VPF_ERR_ARG;
+    if (((uintptr_t)A & 15) || ((uintptr_t)W & 15) || ((uintptr_t)As & 15) || ((uintptr_t)Ws & 15)) return VPF_ERR_ARG;
+    if (lds_a < M || lds_a % 64 != 0 || N % 64 != 0 || lds_a > INT32_MAX / 2) return VPF_ERR_ARG;
+    if (C && (ldc < N || ldc % 8 != 0 || ldc > INT32_MAX / 2)) return VPF_ERR_ARG;
+    if (epilogue == VPF_EPI_BIAS_RESIDUAL && (!residual || !C)) return VPF_ERR_ARG;
+    const bool ln = epilogue == VPF_EPI_LN || epilogue == VPF_EPI_LN_GELU;
+    if (ln && (!row_stats || !colsum)) return VPF_ERR_ARG;
+    if (((uintptr_t)bias & 15) || ((uintptr_t)colsum & 15) || ((uintptr_t)row_stats & 7)) return VPF_ERR_ARG;
+    if (stats_parts < 0 || stats_parts > MX_PARTS || !(ln_eps >= 0.f)) return VPF_ERR_ARG;
+    if (stats_out && (((uintptr_t)stats_out & 7) || epilogue != VPF_EPI_BIAS_RESIDUAL)) return VPF_ERR_ARG;
+    if (vpf_check_out8(C8, ld8, Cs, lds_c, M, N)) return VPF_ERR_ARG;
+    const Out8 o8{C8, reinterpret_cast<uint8_t*>(Cs), (int)ld8, (int)lds_c};
+    const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (tiles > INT32_MAX) return VPF_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid((unsigned)tiles), block(NTHREADS);
+    const int group = vpf_gemm_tile_group();
+    switch (epilogue) {
+        case VPF_EPI_BIAS: VPF_MX8_LAUNCH(VPF_EPI_BIAS); break;
+        case VPF_EPI_BIAS_GELU: VPF_MX8_LAUNCH(VPF_EPI_BIAS_GELU); break;
+        case VPF_EPI_BIAS_RESIDUAL: VPF_MX8_LAUNCH(VPF_EPI_BIAS_RESIDUAL); break;
+        case VPF_EPI_LN: VPF_MX8_LAUNCH(VPF_EPI_LN); break;
+        case VPF_EPI_LN_GELU: VPF_MX8_LAUNCH(VPF_EPI_LN_GELU); break;
+        default: return VPF_ERR_ARG;   // EPI_PATCH: the patch embedding stays bf16 (K = 3 p^2, 0.7 % of FLOPs)
+    }
+    VPF_RETURN_LAUNCH();
+}
+
+VPF_API int vpf_quantize_mx8(const uint16_t* X, int64_t ldx, int64_t rows, int64_t K, int64_t out_stride,
+                             uint8_t* X8, int64_t ld8, uint32_t* S, int64_t lds, void* stream) {
+    if (rows <= 0 || K <= 0 || K % 128 != 0 || ldx < K || ldx % 8 != 0 || out_stride < 1) return VPF_ERR_ARG;
+    if (!X || !X8 || !S || ((uintptr_t)X & 15) || ((uintptr_t)X8 & 7) || ((uintptr_t)S & 3)) return VPF_ERR_ARG;
+    if (ld8 < K || ld8 % 8 != 0 || lds < (rows - 1) * out_stride + 1 || lds % 64 != 0 || lds > INT32_MAX / 4)
+        return VPF_ERR_ARG;
+    const int64_t total = rows * (K / 8);
+    const int64_t blocks = (total + 255) / 256;
+    if (blocks > INT32_MAX || K > 65536) return VPF_ERR_ARG;
+    hipLaunchKernelGGL(k_quantize_mx8, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const bf16_t*>(X), ldx, rows, (int)K, out_stride, X8, ld8,
+                       reinterpret_cast<uint8_t*>(S), lds);
+    VPF_RETURN_LAUNCH();
+}

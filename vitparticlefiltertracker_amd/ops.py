@@ -100,7 +100,8 @@ def _rows(t: torch.Tensor, what: str):
     return t.shape[0], t.stride(0)
 
 
-def _gemm(a, w, bias, residual, pos, patch_rows, row_stats, colsum, epilogue, out, stats_parts, ln_eps, stats_out):
+def _gemm(a, w, bias, residual, pos, patch_rows, row_stats, colsum, epilogue, out, stats_parts, ln_eps, stats_out,
+          q8=None, s8=None):
     _dev(w, bias, pos, row_stats, colsum, stats_out)
     for t in (a, out, residual):
         if t is not None:
@@ -127,8 +128,10 @@ def _gemm(a, w, bias, residual, pos, patch_rows, row_stats, colsum, epilogue, ou
             R = (M // patch_rows) * (patch_rows + 1) if epilogue == _lib.VPF_EPI_PATCH else M
             _chk(stats_out.dtype == _F32 and stats_out.numel() >= ((N + 63) // 64) * R * 2,
                  "gemm: stats_out f32[ceil(N/64)][rows][2]")
+        ld8, lds = _mx8_out(q8, s8, (M // patch_rows) * (patch_rows + 1) if epilogue == _lib.VPF_EPI_PATCH else M, N)
         call("vpf_gemm_bf16", ptr(a), lda, ptr(w), ptr(bias), ptr(residual), ptr(pos), patch_rows, ptr(row_stats),
-             ptr(colsum), ptr(out), ldc, M, N, K, epilogue, stats_parts, ln_eps, ptr(stats_out), stream_ptr())
+             ptr(colsum), ptr(out), ldc, M, N, K, epilogue, stats_parts, ln_eps, ptr(stats_out), ptr(q8), ld8, ptr(s8),
+             lds, stream_ptr())
     else:
         _chk(stats_parts == 0 and stats_out is None, "gemm: statistics planes are a bf16-path feature")
         call("vpf_gemm_f32", ptr(a), lda, ptr(w), ptr(bias), ptr(residual), ptr(pos), patch_rows, ptr(row_stats),
@@ -158,6 +161,155 @@ def gemm_stats_(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: 
     output: `stats_out` [ceil(N/64)][rows][2] f32, per row {sum, sumsq} of the stored bf16 values over each
     64-column block (rows = output rows; token rows for EPI_PATCH, whose CLS rows cls_rows_stats_ fills)."""
     _gemm(a, w, bias, residual, pos, patch_rows, None, None, epilogue, out, 0, 0.0, stats_out)
+
+
+# ---------------------------------------------------------------------------------------------- MX8 (fp8 path)
+# An MX8 tensor is a pair (q, s): q uint8[rows][K] (e4m3fn codes; a row-strided view is allowed) and s int32
+# [K/128][lds] scale planes (e8m0 bytes in 64-row bricks, vpf.h "MX8 operands"), lds = rows rounded up to 64.
+
+def mx8_empty(rows: int, K: int, device, lds_rows: Optional[int] = None):
+    """Allocate an MX8 operand for `rows` rows of K values (scale planes for lds_rows >= rows rows)."""
+    _chk(K % 128 == 0, "mx8: K % 128 == 0")
+    lds = ((max(rows, lds_rows or 0) + 63) // 64) * 64
+    return (torch.empty(rows, K, device=device, dtype=torch.uint8),
+            torch.empty(K // 128, lds, device=device, dtype=torch.int32))
+
+
+def _mx8_in(q, s, what):
+    _chk(q is not None and s is not None and q.is_cuda and s.is_cuda, f"{what}: MX8 operand on the GPU")
+    _chk(q.dtype == torch.uint8 and s.dtype == torch.int32 and s.dim() == 2 and s.is_contiguous(),
+         f"{what}: MX8 operand = (uint8[rows][K], int32[K/128][lds])")
+    rows, ld = _rows(q, what)
+    _chk(s.shape[0] == q.shape[1] // 128 and s.shape[1] >= rows and s.shape[1] % 64 == 0, f"{what}: scale planes")
+    return rows, ld, s.shape[1]
+
+
+def _mx8_out(q8, s8, rows, N):
+    if q8 is None:
+        _chk(s8 is None, "fp8 output: pass both q8 and s8")
+        return 0, 0
+    _chk(s8 is not None and q8.is_cuda and s8.is_cuda and q8.dtype == torch.uint8 and s8.dtype == torch.int32,
+         "fp8 output: (uint8, int32) MX8 pair")
+    qr, ld8 = _rows(q8, "fp8 output")
+    _chk(qr >= rows and q8.shape[1] >= N and s8.is_contiguous() and s8.shape[0] == N // 128
+         and s8.shape[1] >= rows and s8.shape[1] % 64 == 0, "fp8 output: shape / scale planes")
+    return ld8, s8.shape[1]
+
+
+@torch.library.custom_op("vpf::gemm_q8_", mutates_args={"out", "stats_out", "q8", "s8"}, device_types="cuda")
+def gemm_q8_(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: Optional[torch.Tensor],
+             pos: Optional[torch.Tensor], patch_rows: int, epilogue: int, out: torch.Tensor, stats_out: torch.Tensor,
+             q8: torch.Tensor, s8: torch.Tensor) -> None:
+    """gemm_stats_ (bf16 residual-stream producer: EPI_BIAS_RESIDUAL / EPI_PATCH) that also writes an MX8 copy
+    (q8, s8) of its bf16 output — the A operand of the fp8 path's following gemm_mx8."""
+    _gemm(a, w, bias, residual, pos, patch_rows, None, None, epilogue, out, 0, 0.0, stats_out, q8, s8)
+
+
+def _gemm_mx8(a8, as8, w8, ws8, bias, residual, row_stats, colsum, epilogue, out, q8, s8, stats_parts, ln_eps,
+              stats_out):
+    _dev(bias, row_stats, colsum, stats_out, w8, ws8)
+    M, lda, lds_a = _mx8_in(a8, as8, "gemm_mx8 a")
+    N, K = w8.shape
+    _chk(a8.shape[1] == K and ws8.shape == (K // 128, N) and w8.dtype == torch.uint8 and ws8.dtype == torch.int32,
+         "gemm_mx8: w = (uint8[N][K], int32[K/128][N])")
+    _chk(bias.numel() == N and bias.dtype == _F32, "gemm_mx8: bias f32[N]")
+    ldc = 0
+    if out is not None:
+        Mo, ldc = _rows(out, "gemm_mx8 out")
+        _chk(out.is_cuda and out.dtype == _BF16 and Mo == M and out.shape[1] == N, "gemm_mx8: out bf16[M][N]")
+    if residual is not None:
+        _chk(_rows(residual, "gemm_mx8 residual") == (M, ldc), "gemm_mx8: residual must match out's layout")
+    if epilogue in (_lib.VPF_EPI_LN, _lib.VPF_EPI_LN_GELU):
+        _chk(row_stats is not None and row_stats.numel() >= 2 * M * max(stats_parts, 1) and colsum is not None
+             and colsum.numel() == N, "gemm_mx8: LN epilogue needs row_stats [max(P,1)][M][2] and colsum[N]")
+    if stats_out is not None:
+        _chk(stats_out.dtype == _F32 and stats_out.numel() >= ((N + 63) // 64) * M * 2,
+             "gemm_mx8: stats_out f32[ceil(N/64)][M][2]")
+    ld8, lds = _mx8_out(q8, s8, M, N)
+    call("vpf_gemm_mx8", ptr(a8), lda, ptr(as8), lds_a, ptr(w8), ptr(ws8), ptr(bias), ptr(residual), ptr(row_stats),
+         ptr(colsum), ptr(out), ldc, ptr(q8), ld8, ptr(s8), lds, M, N, K, epilogue, stats_parts, ln_eps, ptr(stats_out),
+         stream_ptr())
+
+
+@torch.library.custom_op("vpf::gemm_mx8", mutates_args={"out"}, device_types="cuda")
+def gemm_mx8(a8: torch.Tensor, as8: torch.Tensor, w8: torch.Tensor, ws8: torch.Tensor, bias: torch.Tensor,
+             residual: Optional[torch.Tensor], row_stats: Optional[torch.Tensor], colsum: Optional[torch.Tensor],
+             epilogue: int, out: torch.Tensor, stats_parts: int = 0, ln_eps: float = 0.0) -> None:
+    """fp8 path (configs[4]): out(bf16) = epilogue(value(a8, as8) . value(w8, ws8)^T) on block-scaled MFMA.
+    Epilogues and LN statistics as `gemm` (colsum = row sums of value(w8); stats_parts <= 13)."""
+    _gemm_mx8(a8, as8, w8, ws8, bias, residual, row_stats, colsum, epilogue, out, None, None, stats_parts, ln_eps,
+              None)
+
+
+@torch.library.custom_op("vpf::gemm_mx8_q8_", mutates_args={"q8", "s8"}, device_types="cuda")
+def gemm_mx8_q8_(a8: torch.Tensor, as8: torch.Tensor, w8: torch.Tensor, ws8: torch.Tensor, bias: torch.Tensor,
+                 row_stats: Optional[torch.Tensor], colsum: Optional[torch.Tensor], epilogue: int, q8: torch.Tensor,
+                 s8: torch.Tensor, stats_parts: int = 0, ln_eps: float = 0.0) -> None:
+    """gemm_mx8 whose output is MX8 only (q8, s8): the bf16 epilogue values quantised in the epilogue (FC1 ->
+    the A operand of FC2); no bf16 output is written."""
+    _gemm_mx8(a8, as8, w8, ws8, bias, None, row_stats, colsum, epilogue, None, q8, s8, stats_parts, ln_eps, None)
+
+
+@torch.library.custom_op("vpf::gemm_mx8_res_", mutates_args={"out", "stats_out", "q8", "s8"}, device_types="cuda")
+def gemm_mx8_res_(a8: torch.Tensor, as8: torch.Tensor, w8: torch.Tensor, ws8: torch.Tensor, bias: torch.Tensor,
+                  out: torch.Tensor, stats_out: torch.Tensor, q8: torch.Tensor, s8: torch.Tensor) -> None:
+    """Residual-stream producer on the fp8 path (FC2): out += value(a8) value(w8)^T + bias in place (bf16), plus
+    its statistics planes and its MX8 copy (q8, s8) for the next block's LN-folded gemm_mx8."""
+    _gemm_mx8(a8, as8, w8, ws8, bias, out, None, None, _lib.VPF_EPI_BIAS_RESIDUAL, out, q8, s8, 0, 0.0, stats_out)
+
+
+@torch.library.custom_op("vpf::quantize_mx8_", mutates_args={"q8", "s8"}, device_types="cuda")
+def quantize_mx8_(x: torch.Tensor, out_stride: int, q8: torch.Tensor, s8: torch.Tensor) -> None:
+    """MX8 quantisation of bf16 rows: row r of the (row-strided) view x -> row r*out_stride of (q8, s8)."""
+    _chk(x.is_cuda and x.dtype == _BF16, "quantize_mx8_: bf16 rows on the GPU")
+    rows, ldx = _rows(x, "quantize_mx8_ x")
+    K = x.shape[1]
+    _chk(q8.is_cuda and s8.is_cuda and q8.dtype == torch.uint8 and s8.dtype == torch.int32 and s8.is_contiguous(),
+         "quantize_mx8_: (uint8, int32) output pair")
+    qr, ld8 = _rows(q8, "quantize_mx8_ q8")
+    _chk(qr >= (rows - 1) * out_stride + 1 and q8.shape[1] >= K and s8.shape[0] == K // 128,
+         "quantize_mx8_: output shape")
+    call("vpf_quantize_mx8", ptr(x), ldx, rows, K, out_stride, ptr(q8), ld8, ptr(s8), s8.shape[1], stream_ptr())
+
+
+_E4M3 = None
+
+
+def e4m3_table(device) -> torch.Tensor:
+    """float32[256]: the OCP e4m3fn value of every byte (NaN for 0x7f / 0xff)."""
+    global _E4M3
+    if _E4M3 is None:
+        v = []
+        for b in range(256):
+            sgn = -1.0 if b & 0x80 else 1.0
+            e, m = (b >> 3) & 15, b & 7
+            if e == 15 and m == 7:
+                v.append(float("nan"))
+            elif e == 0:
+                v.append(sgn * m / 8.0 * 2.0 ** -6)
+            else:
+                v.append(sgn * (1.0 + m / 8.0) * 2.0 ** (e - 7))
+        _E4M3 = torch.tensor(v, dtype=torch.float32)
+    return _E4M3.to(device)
+
+
+def mx8_scale_bytes(s8: torch.Tensor, rows: int) -> torch.Tensor:
+    """int32[rows][K/32]: the e8m0 scale byte of every (row, 32-value block) of an MX8 operand's planes."""
+    T, lds = s8.shape
+    b = s8.contiguous().view(torch.uint8).view(T, lds * 4)
+    r = torch.arange(rows, device=s8.device)
+    kb = torch.arange(4, device=s8.device)
+    idx = (((r >> 6) * 64 + (r & 15))[:, None] + kb[None, :] * 16) * 4 + ((r >> 4) & 3)[:, None]   # [rows][4]
+    out = b[:, idx.reshape(-1)].view(T, rows, 4).permute(1, 0, 2).reshape(rows, T * 4)
+    return out.to(torch.int32)
+
+
+def mx8_dequantize(q8: torch.Tensor, s8: torch.Tensor) -> torch.Tensor:
+    """float32[rows][K] values of an MX8 operand (setup-time use: the LN-fold colsum of fp8 weights; tests)."""
+    rows, K = q8.shape
+    vals = e4m3_table(q8.device)[q8.long()]
+    sc = torch.exp2(mx8_scale_bytes(s8, rows).float() - 127.0)
+    return vals * sc.repeat_interleave(32, dim=1)[:, :K]
 
 
 @torch.library.custom_op("vpf::row_stats", mutates_args={"out"}, device_types="cuda")
