@@ -32,7 +32,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec @ 4096 particles, ViT-B/16 224px; 1/2/4/8 MI355X scaling"
-PEAK_BF16_TFLOPS = 2500.0
+PEAK_BF16_TFLOPS = 2500.0     # dense bf16 MFMA, /opt/skills/guides/MI355X_MICROARCH.md (Matrix cores)
+PEAK_FP8_TFLOPS = 5000.0      # dense block-scaled e4m3 MFMA (same table), the fp8 path's GEMMs
 
 
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
@@ -60,7 +61,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--particles", type=int, default=4096, help="global particle count")
     ap.add_argument("--arch", default="vit_base_patch16_224")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
+                    help="fp8: MX-fp8 QKV / FC1 / FC2 GEMMs (configs[4])")
+    ap.add_argument("--frame", default="224x224", help="synthetic source frame HxW (configs[4]: 1080x1920)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--kernel-frames", type=int, default=2, help="eager frames timed per kernel (roofline)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (s); 0 = skip")
@@ -137,7 +140,8 @@ def main() -> int:
     cfg = load_config({"model": {"arch": args.arch, "dtype": args.dtype}, "particles": {"num": args.particles}})
     arch = ARCHS[args.arch]
     n_frames = 1 + args.warmup + args.steps + args.kernel_frames
-    clip = synthetic_clip(n_frames)
+    fh, fw = (int(v) for v in args.frame.lower().split("x"))
+    clip = synthetic_clip(n_frames, fh, fw)
     frames = [torch.from_numpy(f).to(dev) for f in clip]          # resident in HBM before timing
     tr = Tracker(cfg, device=dev, rank=rank, world_size=world, use_graph=not args.no_graph)
     tr.init(frames[0], cfg["input"]["bbox0"])
@@ -183,7 +187,9 @@ def main() -> int:
             v["tflops"] = flops[name] / (v["avg_ms"] * 1e-3) / 1e12
     dom = max((n for n in flops if n.startswith("gemm") and n in ks), key=lambda n: ks[n]["total_ms"])
     ach = ks[dom]["tflops"]
-    traffic, traffic_src = pmc_traffic(args.arch, n_loc, dom)
+    traffic, traffic_src = pmc_traffic(args.arch, n_loc, dom) if args.dtype == "bf16" else (None, None)
+    # the dominant GEMM's MFMA peak: dense bf16, or dense MX-fp8 for the fp8 path's block-scaled GEMMs
+    peak = PEAK_FP8_TFLOPS if args.dtype == "fp8" and dom in ("gemm_qkv", "gemm_fc1", "gemm_fc2") else PEAK_BF16_TFLOPS
     gflop_frame = arch.gflop_per_crop() * args.particles
     line = {
         "metric": METRIC,
@@ -196,14 +202,15 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "bf16" if args.dtype == "bf16" else "f32",
-        "data": "synthetic: u8 224x224 frames (uniform-noise background, moving 64x64 textured target), "
+        "dtype": {"bf16": "bf16", "fp32": "f32", "fp8": "fp8-e4m3(MX)+bf16"}[args.dtype],
+        "data": f"synthetic: u8 {fh}x{fw} frames (uniform-noise background, moving 64x64 textured target), "
                 "seeded random-init ViT weights (no pretrained checkpoint offline)",
-        "config": {"workload": f"{args.particles} particles, {args.arch} {args.dtype}, full tracking step per frame",
-                   "particles": args.particles, "particles_per_gpu": n_loc, "arch": args.arch,
+        "config": {"workload": f"{args.particles} particles, {args.arch} {args.dtype}, {fh}x{fw} frames, "
+                               "full tracking step per frame",
+                   "particles": args.particles, "particles_per_gpu": n_loc, "arch": args.arch, "frame": [fh, fw],
                    "hip_graph": not args.no_graph, "parallelism": f"particle-shard x{world}"},
-        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "avg_launch_ms": round(ks[dom]["avg_ms"], 4),
                      "flop_per_launch": flops[dom]},

@@ -31,7 +31,9 @@ def _crops(arch, n, seed=0):
 
 @pytest.mark.parametrize("name,dtype,n", [("vit_tiny_patch16_224", "fp32", 5), ("vit_tiny_patch16_224", "bf16", 9),
                                           ("vit_base_patch16_224", "bf16", 3), ("vit_base_patch16_224", "fp32", 2),
-                                          ("vit_large_patch14_336", "bf16", 2), ("vit_large_patch14_336", "fp32", 1)])
+                                          ("vit_large_patch14_336", "bf16", 2), ("vit_large_patch14_336", "fp32", 1),
+                                          ("vit_small_patch16_224", "fp8", 7), ("vit_base_patch16_224", "fp8", 3),
+                                          ("vit_large_patch14_336", "fp8", 2)])
 def test_vit_features_vs_oracle(name, dtype, n):
     from vitparticlefiltertracker_amd.vit import ViTEngine
     arch = ARCHS[name]
@@ -44,13 +46,21 @@ def test_vit_features_vs_oracle(name, dtype, n):
     if dtype == "fp32":
         torch.testing.assert_close(feat, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
     else:
+        # bf16: >= 0.999; fp8 (MX e4m3 weights and GEMM inputs, configs[4]): reported tolerance >= 0.99
         cos = torch.nn.functional.cosine_similarity(feat, ref, dim=1)
-        assert cos.min().item() > 0.999, cos
+        assert cos.min().item() > (0.999 if dtype == "bf16" else 0.99), cos
 
 
-def _tiny_cfg(P, dtype):
-    return load_config({"model": {"arch": "vit_tiny_patch16_224", "dtype": dtype, "weights": {"seed": 3}},
+def _tiny_cfg(P, dtype, arch="vit_tiny_patch16_224"):
+    return load_config({"model": {"arch": arch, "dtype": dtype, "weights": {"seed": 3}},
                         "particles": {"num": P, "seed": 99}})
+
+
+def test_fp8_rejects_unaligned_width():
+    from vitparticlefiltertracker_amd.vit import ViTEngine
+    arch = ARCHS["vit_tiny_patch16_224"]                  # D = 192: not a multiple of the 128-deep MX8 K-tile
+    with pytest.raises(ValueError, match="fp8"):
+        ViTEngine(arch, make_vit_weights(arch, seed=0), "fp8", DEV, 4)
 
 
 def test_tracker_fp32_matches_oracle_end_to_end():
@@ -70,12 +80,14 @@ def test_tracker_fp32_matches_oracle_end_to_end():
         np.testing.assert_allclose(e_gpu, e_ref, rtol=1e-4)
 
 
-@pytest.mark.parametrize("use_graph", [True, False])
-def test_tracker_bf16_weight_injection_bit_exact(use_graph):
+@pytest.mark.parametrize("use_graph,dtype,arch_name", [(True, "bf16", "vit_tiny_patch16_224"),
+                                                        (False, "bf16", "vit_tiny_patch16_224"),
+                                                        (True, "fp8", "vit_small_patch16_224")])
+def test_tracker_bf16_weight_injection_bit_exact(use_graph, dtype, arch_name):
     from vitparticlefiltertracker_amd import Tracker
     P = 256
-    cfg = _tiny_cfg(P, "bf16")
-    arch = ARCHS["vit_tiny_patch16_224"]
+    cfg = _tiny_cfg(P, dtype, arch_name)
+    arch = ARCHS[arch_name]
     w = make_vit_weights(arch, seed=3)
     clip = synthetic_clip(6)
     tr = Tracker(cfg, weights=w, use_graph=use_graph)
@@ -97,10 +109,11 @@ def test_tracker_bf16_weight_injection_bit_exact(use_graph):
         assert Q.sum() > 0
 
 
-def test_tracker_graph_equals_eager():
+@pytest.mark.parametrize("dtype,arch_name", [("bf16", "vit_tiny_patch16_224"), ("fp8", "vit_small_patch16_224")])
+def test_tracker_graph_equals_eager(dtype, arch_name):
     from vitparticlefiltertracker_amd import Tracker
-    cfg = _tiny_cfg(128, "bf16")
-    w = make_vit_weights(ARCHS["vit_tiny_patch16_224"], seed=3)
+    cfg = _tiny_cfg(128, dtype, arch_name)
+    w = make_vit_weights(ARCHS[arch_name], seed=3)
     clip = synthetic_clip(5)
     outs = []
     for g in (True, False):
@@ -108,3 +121,19 @@ def test_tracker_graph_equals_eager():
         tr.init(clip[0], (80, 80, 64, 64))
         outs.append(tr.run(clip[1:]))
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_tracker_fp8_1080p_follows_target():
+    """configs[4] geometry on one GPU at a small particle count: ViT-B/16 fp8, 1080x1920 source frames. The
+    tracked centre stays on the moving target (it moves 2.2 px/frame; tolerance 24 px)."""
+    from vitparticlefiltertracker_amd import Tracker
+    from vitparticlefiltertracker_amd.frames import target_box
+    cfg = load_config({"model": {"arch": "vit_base_patch16_224", "dtype": "fp8"},
+                       "particles": {"num": 512, "seed": 5}})
+    clip = synthetic_clip(6, 1080, 1920, bbox0=(900, 500, 64, 64))
+    tr = Tracker(cfg)
+    tr.init(clip[0], (900, 500, 64, 64))
+    for k, f in enumerate(clip[1:], start=1):
+        x, y, s = tr.track(f)
+        bx, by, bw, bh = target_box(k, (900, 500, 64, 64))
+        assert abs(x - (bx + bw / 2)) < 24 and abs(y - (by + bh / 2)) < 24, (k, x, y)

@@ -70,7 +70,7 @@ ARCHS: Dict[str, ViTArch] = {
 DEFAULTS: Dict[str, Any] = {
     "model": {
         "arch": "vit_base_patch16_224",
-        "dtype": "bf16",                 # bf16 (product) | fp32 (parity mode)
+        "dtype": "bf16",                 # bf16 (product) | fp8 (MX-fp8 encoder GEMMs, configs[4]) | fp32 (parity)
         "weights": {"seed": 0},
         "mean": [0.5, 0.5, 0.5],
         "std": [0.5, 0.5, 0.5],
@@ -114,8 +114,8 @@ def load_config(cfg: Optional[Any] = None) -> Dict[str, Any]:
     arch = out["model"]["arch"]
     if arch not in ARCHS:
         raise ValueError(f"unknown model.arch {arch!r}; known: {sorted(ARCHS)}")
-    if out["model"]["dtype"] not in ("bf16", "fp32"):
-        raise ValueError("model.dtype must be 'bf16' or 'fp32'")
+    if out["model"]["dtype"] not in ("bf16", "fp8", "fp32"):
+        raise ValueError("model.dtype must be 'bf16', 'fp8' or 'fp32'")
     if out["resample"]["method"] != "systematic":
         raise ValueError("only resample.method == 'systematic' is defined (SPEC S7)")
     return out

@@ -16,6 +16,13 @@ HBM layout (bf16 mode, P particles, N tokens, D width, F MLP width):
   h   [P][N][D]   residual stream (bf16)          x   [P][N][D]   LN output / attention output
   qkv [P][N][3D]  (3, heads, 64) column order      hid [P][N][F]   GELU(FC1) (also hosts the im2col patches)
 Weights are [out][in] (K-contiguous rows) bf16 with fp32 biases / LayerNorm affines / cls / pos.
+
+fp8 mode (model.dtype = "fp8", BASELINE.json configs[4]): the QKV, FC1 and FC2 GEMMs (9/12 of the encoder
+FLOPs) run on block-scaled MFMA (vpf_gemm_mx8) with MX-fp8 weights (quantised once from the LN-folded bf16
+weights) and MX-fp8 activations written by the producing epilogues:
+  h8   MX8 copy of h   (patch embed / proj / FC2 epilogues; CLS rows by vpf_quantize_mx8) -> QKV, FC1 A operand
+  hid8 MX8 GELU(FC1)   (FC1 epilogue, no bf16 copy)                                      -> FC2 A operand
+The residual stream h, qkv, the attention and the proj GEMM stay bf16, as does the last block's CLS-row tail.
 """
 from __future__ import annotations
 
@@ -81,7 +88,13 @@ class ViTEngine:
         _lib.lib()  # fail loudly now if libvpf.so is missing
         self.arch = arch
         self.device = torch.device(device)
-        self.dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        if dtype not in ("bf16", "fp8", "fp32"):
+            raise ValueError(f"dtype {dtype!r}: bf16 | fp8 | fp32")
+        self.fp8 = dtype == "fp8"
+        self.dt = torch.float32 if dtype == "fp32" else torch.bfloat16
+        if self.fp8 and (arch.dim % 128 or arch.mlp % 128):
+            raise ValueError(f"fp8 mode needs D and the MLP width divisible by 128 (MX8 K-tiles); {arch.name} has "
+                             f"D = {arch.dim}")
         self.batch = int(batch)
         self.norm_ab = norm_affine(mean, std)
         A = arch
@@ -132,6 +145,17 @@ class ViTEngine:
             else:
                 L["wqkv"], L["bqkv"] = mat(weights[p + "attn.qkv.weight"]), f32(weights[p + "attn.qkv.bias"])
                 L["wfc1"], L["bfc1"] = mat(weights[p + "mlp.fc1.weight"]), f32(weights[p + "mlp.fc1.bias"])
+            if self.fp8:
+                # MX8 copies of the three GEMMs that run on block-scaled MFMA; LN-fold colsums of the
+                # dequantised W' so the fold's algebra holds exactly for the weights the MFMA multiplies
+                for key in ("wqkv", "wfc1", "wfc2"):
+                    q, sc = ops.mx8_empty(L[key].shape[0], L[key].shape[1], dev)
+                    vpf.quantize_mx8_(L[key], 1, q, sc)
+                    L[key + "8"] = (q, sc)
+                for key, ck in (("wqkv", "cqkv"), ("wfc1", "cfc1")):
+                    L[ck + "8"] = ops.mx8_dequantize(*L[key + "8"]).sum(dim=1).contiguous()
+                q, sc = L["wqkv8"]
+                L["wkv8"] = (q[D:], sc[:, D:].contiguous())        # the last block's K | V rows (64-row bricks)
             self.layers.append(L)
         self.ng = f32(weights["norm.weight"])
         self.nb = f32(weights["norm.bias"])
@@ -158,6 +182,11 @@ class ViTEngine:
         self.use_planes = self.fold_ln and self.parts <= 16
         self.planes_flat = torch.empty(self.parts * n * N * 2, device=dev, dtype=torch.float32)
         self.planes_cls_flat = torch.empty(self.parts * n * 2, device=dev, dtype=torch.float32)
+        if self.fp8:
+            self.h8 = ops.mx8_empty(n * N, D, dev)
+            self.hid8 = ops.mx8_empty(n * N, F, dev)
+        # the MX8 consumers read at most 13 statistics planes (LDS budget, vpf_gemm_mx8)
+        self.planes8 = self.use_planes and self.parts <= 13
         self.Q = torch.empty(n, device=dev, dtype=torch.int64)
         self.feat = torch.empty(n, D, device=dev, dtype=torch.float32)
         self.sim = torch.empty(n, device=dev, dtype=torch.float32)
@@ -176,7 +205,15 @@ class ViTEngine:
              A.img_size, A.patch, self.norm_ab, patches)
         h = self.h[:n]
         pl = self.planes(n) if self.use_planes else None
-        if pl is not None:
+        if self.fp8:
+            N = A.tokens
+            pl = pl if pl is not None else self.planes_flat[: self.parts * n * N * 2].view(self.parts, n * N, 2)
+            h8q, h8s = self.h8
+            _run(T, "gemm_patch", vpf.gemm_q8_, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches,
+                 _lib.VPF_EPI_PATCH, h, pl, h8q, h8s)
+            _run(T, "cls_rows", vpf.cls_rows_stats_, h, self.cls, self.pos, pl)
+            _run(T, "cls_q8", vpf.quantize_mx8_, h.view(n, N * A.dim)[:, :A.dim], N, h8q, h8s)
+        elif pl is not None:
             _run(T, "gemm_patch", vpf.gemm_stats_, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches,
                  _lib.VPF_EPI_PATCH, h, pl)
             _run(T, "cls_rows", vpf.cls_rows_stats_, h, self.cls, self.pos, pl)
@@ -231,14 +268,44 @@ class ViTEngine:
         q2 = qkv.view(n * N, 3 * D)
         kv2 = q2[:, D:]                                 # K | V columns of every row
         qc = qkv.view(n, N * 3 * D)[:, :D]             # Q columns of the CLS rows
+        if self.fp8:
+            h8q, h8s = self.h8
+            h8q = h8q[: n * N]
+            hq, hs = self.hid8
+            hq = hq[: n * N]
+
+            def ln_stats8(x):
+                """LN statistics for an MX8 consumer: the planes when it can hold them, else a row_stats pass."""
+                if self.planes8:
+                    return pl, P
+                _run(T, "row_stats", vpf.row_stats, x, eps, st)
+                return st, 0
         for l, L in enumerate(self.layers):
             last = l == len(self.layers) - 1
+            if self.fp8 and not last:
+                s1, p1 = ln_stats8(h2)
+                _run(T, "gemm_qkv", vpf.gemm_mx8, h8q, h8s, *L["wqkv8"], L["bqkv"], None, s1, L["cqkv8"], LNE, q2,
+                     p1, eps)
+                _run(T, "attention", vpf.attention, qkv, A.heads, N, self.x[:n])
+                _run(T, "gemm_proj", vpf.gemm_q8_, x2, L["wproj"], L["bproj"], h2, None, 0, RES, h2, pl, h8q, h8s)
+                s2, p2 = ln_stats8(h2)
+                _run(T, "gemm_fc1", vpf.gemm_mx8_q8_, h8q, h8s, *L["wfc18"], L["bfc1"], s2, L["cfc18"], LNG, hq, hs,
+                     p2, eps)
+                _run(T, "gemm_fc2", vpf.gemm_mx8_res_, hq, hs, *L["wfc28"], L["bfc2"], h2, pl, h8q, h8s)
+                continue
             # the last block's attention reads only the CLS query: K, V for every row, Q for the CLS rows
             if fold:
                 s1, p1 = ln_stats(h2, st, pl)
                 if not last:
                     _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, s1, L["cqkv"], LNE, q2,
                          p1, eps)
+                elif self.fp8:
+                    s8, p8 = ln_stats8(h2)
+                    _run(T, "gemm_kv", vpf.gemm_mx8, h8q, h8s, *L["wkv8"], L["bqkv"][D:], None, s8, L["cqkv8"][D:],
+                         LNE, kv2, p8, eps)
+                    _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # the CLS rows' {mean, rstd}
+                    _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc,
+                         L["cqkv"][:D], LNE, qc)
                 else:
                     _run(T, "gemm_kv", vpf.gemm, h2, L["wqkv"][D:], L["bqkv"][D:], None, None, 0, s1, L["cqkv"][D:],
                          LNE, kv2, p1, eps)
