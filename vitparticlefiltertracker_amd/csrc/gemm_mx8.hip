@@ -13,7 +13,8 @@
 // lane-linear LDS image and 16-B DMA pieces, plus 1 KiB of scale words per operand (one 16-B piece per lane
 // of one wave). Per K-tile a wave reads 24 ds_read_b128 (two per fragment: its 32-byte K-block) and 3 scale
 // words (op_sel picks a fragment's byte), then issues 32 MFMAs (each 2x the cycles of a 16x16x32 bf16 MFMA for 4x the K). Two-stage ring
-// (2 x 66 KiB) + 28 KiB epilogue operands (bias | colsum | up to MX_PARTS statistics planes) = 160 KiB.
+// (2 x 66 KiB) with two K-tiles of lookahead (a buffer is refilled once its K-tile sits in registers) + 28 KiB
+// epilogue operands (bias | colsum | up to MX_PARTS statistics planes) = 160 KiB.
 // Epilogues: gemm_common.h store_wave_tile (bias / LN fold / GELU / residual, statistics planes, optional
 // MX-fp8 copy of the output).
 #include <stdlib.h>
@@ -23,6 +24,21 @@ using namespace vpf;
 using namespace vpf::gemm;
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// LDS fragment reads as inline asm: hipcc's waitcnt pass cannot tell these reads from the in-flight LDS-DMA
+// writes of the other buffer and would drain vmcnt(0) before them (losing the lookahead); the kernel waits
+// for them itself (lgkmcnt(0) tied to the fragment registers, below).
+__device__ __forceinline__ i32x4 lds16(const char* p) {
+    i32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lptr_t)p));
+    return v;
+}
+__device__ __forceinline__ int lds4(const void* p) {
+    int v;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lptr_t)p));
+    return v;
+}
 
 namespace {
 
@@ -74,8 +90,11 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
         offA[i] = (uint32_t)min(row, M - 1 - m0) * (uint32_t)lda + (uint32_t)(lch * 16);
         offB[i] = (uint32_t)min(row, N - 1 - n0) * (uint32_t)K + (uint32_t)(lch * 16);
     }
-    // scale words of rows [m0 + 4 lane, +4): rows past the end read the last valid 16 B (never used)
-    const int sa_row = min(m0 + 4 * lane, lds_a - 4), sb_row = min(n0 + 4 * lane, N - 4);
+    // scale words: waves 0-3 DMA the A rows' 4 x 256 B, waves 4-7 the W rows' (4 B per lane, one piece per wave,
+    // so every wave issues the same 9 pieces per K-tile and the counted waits below are wave-uniform); rows past
+    // the end read the last valid word (never used)
+    const uint32_t* sc_src = wid < 4 ? As + min(m0 + wid * 64 + lane, lds_a - 1) : Ws + min(n0 + (wid - 4) * 64 + lane, N - 1);
+    const int64_t sc_kstride = wid < 4 ? lds_a : N;
     auto stage = [&](int buf, int kt) {
         char* st = smem + buf * STAGE;
         const uint32_t koff = (uint32_t)kt * BK;
@@ -86,12 +105,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
             __builtin_amdgcn_global_load_lds((gptr_t)(Bblk + offB[i] + koff), (lptr_t)(st + TILE_BYTES + g * 1024), 16,
                                              0, 0);
         }
-        if (wid == 0)
-            __builtin_amdgcn_global_load_lds((gptr_t)(As + (int64_t)kt * lds_a + sa_row), (lptr_t)(st + 2 * TILE_BYTES),
-                                             16, 0, 0);
-        if (wid == 1)
-            __builtin_amdgcn_global_load_lds((gptr_t)(Ws + (int64_t)kt * N + sb_row),
-                                             (lptr_t)(st + 2 * TILE_BYTES + SC_BYTES), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gptr_t)(sc_src + kt * sc_kstride), (lptr_t)(st + 2 * TILE_BYTES + wid * 256), 4,
+                                         0, 0);
     };
 
     constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
@@ -128,12 +143,20 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // Two buffers, two K-tiles of lookahead: a K-tile's buffer is refilled as soon as every wave holds that
+    // K-tile's fragments in registers (second barrier), not after its MFMAs — the DMA of K-tile t+2 flies during
+    // K-tile t's MFMAs and all of K-tile t+1. Per wave, the in-flight pieces at the top of step t are K-tile
+    // t+1's 9 (A 4, B 4, one scale piece): a counted vmcnt(9), never a drain inside the loop.
     const int nk = K / BK;
-    stage(0, 0);
+    // The refill is unconditional (past the end it re-reads K-tile nk-1 into the free buffer) so that it stays in
+    // the MFMA basic block and its 9 DMA issues interleave with the MFMAs (sched_group_barrier below).
     load_aux();
+    stage(0, 0);
+    stage(1, min(1, nk - 1));
     for (int kt = 0; kt < nk; ++kt) {
-        __syncthreads();   // K-tile kt landed for every wave; K-tile kt-1's buffer is free
-        if (kt + 1 < nk) stage((kt + 1) & 1, kt + 1);
+        asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // K-tile kt (and the epilogue operands) landed for every wave
+        asm volatile("" ::: "memory");
         const char* st = smem + (kt & 1) * STAGE;
         const char* la = st;
         const char* lb = st + TILE_BYTES;
@@ -144,34 +167,56 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
         // halves), and the scale of K-block b = [32b, 32b+32) comes from lane group b. So a lane reads logical
         // chunks fq and 4+fq of its row, and supplies the scale of block fq: one word per 64-row brick, byte f
         // = fragment f of the brick (mx8_scale_byte).
-        i32x8 a[8], b[4];
+        i32x4 bl[4], bh[4], al[8], ah[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int row = wn * 64 + j * 16 + fr;
             const int sw = (row >> 1) & 7;
-            const int4 lo = *reinterpret_cast<const int4*>(lb + row * 128 + (fq ^ sw) * 16);
-            const int4 hi = *reinterpret_cast<const int4*>(lb + row * 128 + ((4 + fq) ^ sw) * 16);
-            b[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            bl[j] = lds16(lb + row * 128 + (fq ^ sw) * 16);
+            bh[j] = lds16(lb + row * 128 + ((4 + fq) ^ sw) * 16);
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int row = wm * 128 + i * 16 + fr;
             const int sw = (row >> 1) & 7;
-            const int4 lo = *reinterpret_cast<const int4*>(la + row * 128 + (fq ^ sw) * 16);
-            const int4 hi = *reinterpret_cast<const int4*>(la + row * 128 + ((4 + fq) ^ sw) * 16);
-            a[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            al[i] = lds16(la + row * 128 + (fq ^ sw) * 16);
+            ah[i] = lds16(la + row * 128 + ((4 + fq) ^ sw) * 16);
         }
-        const int sb = (int)lbs[wn * 64 + fq * 16 + fr];
-        const int sa0 = (int)las[(2 * wm) * 64 + fq * 16 + fr];
-        const int sa1 = (int)las[(2 * wm + 1) * 64 + fq * 16 + fr];
+        int sb = lds4(lbs + wn * 64 + fq * 16 + fr);
+        int sa0 = lds4(las + (2 * wm) * 64 + fq * 16 + fr);
+        int sa1 = lds4(las + (2 * wm + 1) * 64 + fq * 16 + fr);
+        // the reads have landed (the wait is tied to every fragment register so no use moves above it)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(bl[0]), "+v"(bl[1]), "+v"(bl[2]), "+v"(bl[3]), "+v"(bh[0]), "+v"(bh[1]), "+v"(bh[2]),
+                       "+v"(bh[3]), "+v"(sb), "+v"(sa0), "+v"(sa1)
+                     :: "memory");
+        asm volatile(""
+                     : "+v"(al[0]), "+v"(al[1]), "+v"(al[2]), "+v"(al[3]), "+v"(al[4]), "+v"(al[5]), "+v"(al[6]),
+                       "+v"(al[7]), "+v"(ah[0]), "+v"(ah[1]), "+v"(ah[2]), "+v"(ah[3]), "+v"(ah[4]), "+v"(ah[5]),
+                       "+v"(ah[6]), "+v"(ah[7]));
+        __builtin_amdgcn_s_barrier();   // every wave holds K-tile kt in registers: its buffer is free
+        asm volatile("" ::: "memory");
+        i32x8 a[8], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            b[j] = i32x8{bl[j].x, bl[j].y, bl[j].z, bl[j].w, bh[j].x, bh[j].y, bh[j].z, bh[j].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            a[i] = i32x8{al[i].x, al[i].y, al[i].z, al[i].w, ah[i].x, ah[i].y, ah[i].z, ah[i].w};
+        stage(kt & 1, min(kt + 2, nk - 1));
         // swapped operands as in the bf16 kernel: W fragment as MFMA-A, activation as MFMA-B -> D[n][m]
         mx_col<0>(acc[0], b[0], a, sb, sa0, sa1);
         mx_col<1>(acc[1], b[1], a, sb, sa0, sa1);
         mx_col<2>(acc[2], b[2], a, sb, sa0, sa1);
         mx_col<3>(acc[3], b[3], a, sb, sa0, sa1);
-        __builtin_amdgcn_sched_group_barrier(0x100, 27, 0);   // fragment + scale reads first
-        __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);   // then the 32 MFMAs
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {   // one DMA issue after every 3 MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing refills land before the ring is reused
 
     if constexpr (LN) {
         if (stats_parts > 0 && tid < BM) {   // planes -> {mean, rstd} once per row (see gemm_bf16.hip)
