@@ -138,6 +138,10 @@ int vpf_layernorm_f32(const float* x, int64_t rows, int D, int64_t x_stride, con
  * the last encoder layer whose other rows feed nothing). hd == 64, N <= 640 (f32: N <= 4096, keys streamed through LDS in 128-key chunks). */
 int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd,
                        float scale, int q_rows, void* stream);
+/* fp8 path: vpf_attention_bf16 (all N <= 256 query rows) writing its output as MX8 (out8 / s8: the A operand of
+ * the MX8 proj GEMM, "MX8 operands" at vpf_gemm_mx8; D = H*hd, D % 128 == 0, lds >= B*N) instead of bf16. */
+int vpf_attention_bf16_mx8(const uint16_t* qkv, int64_t B, int N, int H, int hd, float scale, uint8_t* out8,
+                           int64_t ld8, uint32_t* s8, int64_t lds, void* stream);
 int vpf_attention_f32(const float* qkv, float* out, int64_t B, int N, int H, int hd, float scale,
                       int q_rows, void* stream);
 

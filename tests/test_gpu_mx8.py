@@ -292,3 +292,18 @@ def test_mx8_argument_contract():
         w8, ws8 = ops().mx8_empty(128, 128, DEV)
         vpf().gemm_mx8(a8, as8, w8, ws8[:, :128].contiguous(), torch.zeros(128, device=DEV), None, None, None,
                        _lib.VPF_EPI_PATCH, torch.empty(64, 128, device=DEV, dtype=torch.bfloat16))
+
+
+@pytest.mark.parametrize("B,N,H", [(3, 197, 12), (2, 50, 4)])
+def test_attention_mx8_output_matches_quantizer(B, N, H):
+    """fp8 path attention: the MX8 output == quantize_mx8 of the bf16 output of the same kernel, bit for bit."""
+    D = H * 64
+    torch.manual_seed(B * N)
+    qkv = (torch.randn(B, N, 3 * D, device=DEV) * 0.7).to(torch.bfloat16)
+    out = torch.empty(B, N, D, device=DEV, dtype=torch.bfloat16)
+    vpf().attention(qkv, H, N, out)
+    q, s = ops().mx8_empty(B * N, D, DEV)
+    vpf().attention_q8_(qkv, H, q, s)
+    rq, rs = quant(out.view(B * N, D))
+    assert torch.equal(q, rq)
+    assert torch.equal(ops().mx8_scale_bytes(s, B * N), ops().mx8_scale_bytes(rs, B * N))

@@ -18,6 +18,7 @@
 #include <cstdlib>
 
 #include "vpf_common.h"
+#include "mx8.h"
 #include "../../include/vpf.h"
 
 using namespace vpf;
@@ -265,9 +266,12 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // measured 3-4 % faster than per-chunk barriers (1, 2, 3, 4: 1.223 / 1.210 / 1.196 / 1.178 ms at 4096 x 12
 // heads, profiles/r1_gemm_lab/attn_cpb.txt): each barrier puts all 8 waves back in lockstep.
 constexpr int PIPE_CPB = 4;
-template <int CPB>
+// OUT8: the output is written as MX8 (the fp8 path's proj A operand) instead of bf16: the same packed bf16
+// values, quantised per 32-dim block (a block = 16 dims of a lane + 16 of its partner half-wave lane).
+template <int CPB, bool OUT8 = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_pipe(
-    const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows) {
+    const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows,
+    uint8_t* __restrict__ out8 = nullptr, int ld8 = 0, uint8_t* __restrict__ s8 = nullptr, int lds8 = 0) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int NP = (N + 31) & ~31;
     const int NT = NP >> 5;              // 32-key chunks
@@ -347,6 +351,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
         const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
         ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
+    if constexpr (OUT8) {
+        // lane (l32, hh) holds dims 16k + 8hh .. +7 (k = 0..3): block b = dims 32b .. 32b+31 is ov[2b], ov[2b+1]
+        // of this lane and of its partner lane l32 + 32 (1 - hh)
+        int E[2];
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2) {
+            uint32_t am = max(mx8_amax8(ov[2 * b2]), mx8_amax8(ov[2 * b2 + 1]));
+            am = max(am, (uint32_t)__shfl_xor((int)am, 32, 64));
+            E[b2] = mx8_block_exp(am);
+        }
+        if (q < q_rows) {
+            const int64_t r = row0 + q;
+            uint8_t* orow = out8 + r * ld8 + h * HD + 8 * hh;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) *reinterpret_cast<uint2*>(orow + 16 * k) = mx8_pack8(ov[k], E[k >> 1]);
+            s8[mx8_scale_byte(r, h * HD + 32 * hh, lds8)] = (uint8_t)(E[hh] + 127);
+        }
+        return;
     }
     if (q < q_rows) {
         bf16_t* orow = out + (row0 + q) * D + h * HD + 8 * hh;
@@ -562,6 +585,28 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     }
     hipLaunchKernelGGL(k_attn_bf16, dim3((unsigned)(B * H)), dim3(threads), lds, (hipStream_t)stream, qkv, out, N,
                        H, scale_log2, q_rows);
+    VPF_RETURN_LAUNCH();
+}
+
+VPF_API int vpf_attention_bf16_mx8(const uint16_t* qkv, int64_t B, int N, int H, int hd, float scale, uint8_t* out8,
+                                   int64_t ld8, uint32_t* s8, int64_t lds, void* stream) {
+    const int64_t D = (int64_t)H * HD;
+    if (B < 0 || N <= 0 || N > 256 || H <= 0 || hd != HD || B * H > INT32_MAX || D % 128 != 0) return VPF_ERR_ARG;
+    if (!qkv || !out8 || !s8 || ld8 < D || ld8 % 8 != 0 || ((uintptr_t)out8 & 7) || lds % 64 != 0 ||
+        lds < B * N || ld8 > INT32_MAX || lds > INT32_MAX / 4)
+        return VPF_ERR_ARG;
+    if (B == 0) return 0;
+    const int NP = (N + 31) & ~31;
+    const size_t lds_bytes = (size_t)NP * ROWB * 2;
+    static bool attr = false;   // benign race: idempotent attribute set
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_attn_bf16_pipe<PIPE_CPB, true>), dim3((unsigned)(B * H)), dim3(512), lds_bytes,
+                       (hipStream_t)stream, qkv, (bf16_t*)nullptr, N, H, scale * 1.44269504088896341f, N, out8, (int)ld8,
+                       reinterpret_cast<uint8_t*>(s8), (int)lds);
     VPF_RETURN_LAUNCH();
 }
 

@@ -346,6 +346,21 @@ def attention(qkv: torch.Tensor, heads: int, q_rows: int, out: torch.Tensor) -> 
     call(name, ptr(qkv), ptr(out), B, N, heads, hd, hd ** -0.5, q_rows, stream_ptr())
 
 
+@torch.library.custom_op("vpf::attention_q8_", mutates_args={"q8", "s8"}, device_types="cuda")
+def attention_q8_(qkv: torch.Tensor, heads: int, q8: torch.Tensor, s8: torch.Tensor) -> None:
+    """H6 on the fp8 path: every query row (N <= 256), output written as MX8 (q8, s8) — the proj GEMM's A
+    operand — instead of bf16."""
+    _dev(qkv, s8)
+    _chk(qkv.dtype == _BF16 and q8.is_cuda and q8.dtype == torch.uint8 and s8.dtype == torch.int32,
+         "attention_q8_: bf16 qkv, MX8 (uint8, int32) output")
+    B, N, D3 = qkv.shape
+    D = D3 // 3
+    rows, ld8 = _rows(q8, "attention_q8_ q8")
+    _chk(rows >= B * N and q8.shape[1] >= D and s8.shape[0] == D // 128, "attention_q8_: output shape")
+    call("vpf_attention_bf16_mx8", ptr(qkv), B, N, heads, D // heads, (D // heads) ** -0.5, ptr(q8), ld8, ptr(s8),
+         s8.shape[1], stream_ptr())
+
+
 @torch.library.custom_op("vpf::cls_weight", mutates_args={"Q", "feat", "sim"}, device_types="cuda")
 def cls_weight(tokens: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, tmpl: torch.Tensor,
                lam: float, bits: int, Q: torch.Tensor, feat: Optional[torch.Tensor],

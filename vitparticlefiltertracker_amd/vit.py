@@ -17,12 +17,14 @@ HBM layout (bf16 mode, P particles, N tokens, D width, F MLP width):
   qkv [P][N][3D]  (3, heads, 64) column order      hid [P][N][F]   GELU(FC1) (also hosts the im2col patches)
 Weights are [out][in] (K-contiguous rows) bf16 with fp32 biases / LayerNorm affines / cls / pos.
 
-fp8 mode (model.dtype = "fp8", BASELINE.json configs[4]): the QKV, FC1 and FC2 GEMMs (9/12 of the encoder
-FLOPs) run on block-scaled MFMA (vpf_gemm_mx8) with MX-fp8 weights (quantised once from the LN-folded bf16
-weights) and MX-fp8 activations written by the producing epilogues:
+fp8 mode (model.dtype = "fp8", BASELINE.json configs[4]): the QKV, proj, FC1 and FC2 GEMMs run on
+block-scaled MFMA (vpf_gemm_mx8) with MX-fp8 weights (quantised once from the LN-folded bf16 weights) and
+MX-fp8 activations written by the producing kernels:
   h8   MX8 copy of h   (patch embed / proj / FC2 epilogues; CLS rows by vpf_quantize_mx8) -> QKV, FC1 A operand
+  x8   MX8 attention output (vpf_attention_bf16_mx8; shares hid8's storage)              -> proj A operand
   hid8 MX8 GELU(FC1)   (FC1 epilogue, no bf16 copy)                                      -> FC2 A operand
-The residual stream h, qkv, the attention and the proj GEMM stay bf16, as does the last block's CLS-row tail.
+The residual stream h, qkv and the attention arithmetic stay bf16, as does the last block's CLS-row tail (and,
+for N > 256, the attention output and proj).
 """
 from __future__ import annotations
 
@@ -148,7 +150,7 @@ class ViTEngine:
             if self.fp8:
                 # MX8 copies of the three GEMMs that run on block-scaled MFMA; LN-fold colsums of the
                 # dequantised W' so the fold's algebra holds exactly for the weights the MFMA multiplies
-                for key in ("wqkv", "wfc1", "wfc2"):
+                for key in ("wqkv", "wproj", "wfc1", "wfc2"):
                     q, sc = ops.mx8_empty(L[key].shape[0], L[key].shape[1], dev)
                     vpf.quantize_mx8_(L[key], 1, q, sc)
                     L[key + "8"] = (q, sc)
@@ -272,6 +274,7 @@ class ViTEngine:
             h8q, h8s = self.h8
             h8q = h8q[: n * N]
             hq, hs = self.hid8
+            hq8d = hq.view(-1)[: n * N * D].view(n * N, D)   # the attention's MX8 output (x8) shares hid8's storage
             hq = hq[: n * N]
 
             def ln_stats8(x):
@@ -286,8 +289,14 @@ class ViTEngine:
                 s1, p1 = ln_stats8(h2)
                 _run(T, "gemm_qkv", vpf.gemm_mx8, h8q, h8s, *L["wqkv8"], L["bqkv"], None, s1, L["cqkv8"], LNE, q2,
                      p1, eps)
-                _run(T, "attention", vpf.attention, qkv, A.heads, N, self.x[:n])
-                _run(T, "gemm_proj", vpf.gemm_q8_, x2, L["wproj"], L["bproj"], h2, None, 0, RES, h2, pl, h8q, h8s)
+                if N <= 256:   # attention writes MX8 (into hid8's storage, free until FC1) -> MX8 proj
+                    x8q, x8s = hq8d, hs[: D // 128]
+                    _run(T, "attention", vpf.attention_q8_, qkv, A.heads, x8q, x8s)
+                    _run(T, "gemm_proj", vpf.gemm_mx8_res_, x8q, x8s, *L["wproj8"], L["bproj"], h2, pl, h8q, h8s)
+                else:
+                    _run(T, "attention", vpf.attention, qkv, A.heads, N, self.x[:n])
+                    _run(T, "gemm_proj", vpf.gemm_q8_, x2, L["wproj"], L["bproj"], h2, None, 0, RES, h2, pl, h8q,
+                         h8s)
                 s2, p2 = ln_stats8(h2)
                 _run(T, "gemm_fc1", vpf.gemm_mx8_q8_, h8q, h8s, *L["wfc18"], L["bfc1"], s2, L["cfc18"], LNG, hq, hs,
                      p2, eps)
