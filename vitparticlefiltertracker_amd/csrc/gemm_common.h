@@ -81,11 +81,9 @@ struct Out8 {
 // then each lane sums the 8 partials of two rows and stores them with one 16-B store; no cross-wave step.
 // OUT8: the same bf16 values are also MX-quantised (mx8_quant8: a 32-column block is one DPP quad of lanes)
 // and stored as 8-B element pieces plus one scale byte per row and block.
-template <int EPI, bool OUT8>
-__device__ __forceinline__ void store_wave_tile(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
-                                                int m0, int n0, int lane, const bf16_t* residual,
-                                                const float* __restrict__ pos, int g2, bf16_t* C, int ldc, int M,
-                                                int N, float* stats_out, int stats_rows, Out8 o8) {
+template <int EPI>
+__device__ __forceinline__ void epi_to_image(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
+                                             int lane) {
     constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
     const int fr = lane & 15, fq = lane >> 4;
     float4 bv[4], cv[4];
@@ -130,6 +128,14 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
                 make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
         }
     }
+}
+
+template <int EPI, bool OUT8>
+__device__ __forceinline__ void store_wave_tile(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
+                                                int m0, int n0, int lane, const bf16_t* residual,
+                                                const float* __restrict__ pos, int g2, bf16_t* C, int ldc, int M,
+                                                int N, float* stats_out, int stats_rows, Out8 o8) {
+    epi_to_image<EPI>(img, aux, acc, wm, wn, lane);
     const int c16 = lane & 7;
     uint4 res[16];
     if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
@@ -240,6 +246,58 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
             }
         }
     }
+}
+
+// fp8-only output (no bf16 copy: FC1 -> FC2's A operand). Same image as store_wave_tile, read back 32 B per
+// lane (16 consecutive columns: 4 lanes per 64-column row, 8 iterations) so every element store is 16 B, and a
+// 32-column block is a lane pair (one DPP step). The wave owns whole scale words (its 128 rows are two 64-row
+// bricks, its 64 columns two K-blocks of one plane): the bytes are gathered in the image, then one dword store
+// per lane writes all 64 words.
+template <int EPI>
+__device__ __forceinline__ void store_wave_tile_q8(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
+                                                   int m0, int n0, int lane, int M, int N, Out8 o8) {
+    epi_to_image<EPI>(img, aux, acc, wm, wn, lane);
+    __builtin_amdgcn_wave_barrier();
+    const int cc = lane & 3;   // 16-column group of the wave's 64 columns
+    uint32_t e8[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int row = it * 16 + (lane >> 2);
+        uint4 h[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c16 = 2 * cc + u;
+            uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+            if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+            h[u] = v;
+        }
+        uint32_t am = max(mx8_amax8(h[0]), mx8_amax8(h[1]));
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0xB1, 0xF, 0xF, false));   // lane pair = block
+        const int E = mx8_block_exp(am);
+        e8[it] = (uint32_t)(E + 127);
+        const uint2 q0 = mx8_pack8(h[0], E), q1 = mx8_pack8(h[1], E);
+        const int m = m0 + wm * 128 + row;
+        const int n = n0 + wn * 64 + cc * 16;
+        if (m < M && n < N) *reinterpret_cast<uint4*>(o8.q + (int64_t)m * o8.ldq + n) = make_uint4(q0.x, q0.y, q1.x, q1.y);
+    }
+    // scale bytes -> the wave's 64 words (word w = brick (w >> 5), block (w >> 4) & 1, row r16 = w & 15; byte f =
+    // rows 16f + r16 of the brick), staged in image bytes no lane reads any more
+    __builtin_amdgcn_wave_barrier();
+    if ((lane & 1) == 0) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int row = it * 16 + (lane >> 2);
+            const int w = (row >> 6) * 32 + (cc >> 1) * 16 + (row & 15);
+            img[w * 4 + ((row >> 4) & 3)] = (char)e8[it];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t word = *reinterpret_cast<const uint32_t*>(img + lane * 4);
+    const int nb = n0 + wn * 64;
+    const int R = m0 + wm * 128 + (lane >> 5) * 64;   // brick row base
+    if (nb < N && R < o8.lds)
+        reinterpret_cast<uint32_t*>(o8.s)[(int64_t)(nb >> 7) * o8.lds + R + (((nb >> 5) & 3) + ((lane >> 4) & 1)) * 16 +
+                                          (lane & 15)] = word;
 }
 
 }  // namespace gemm

@@ -234,8 +234,11 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
     }
     __syncthreads();   // the ring is free: 8 x 16 KiB epilogue images
     float* prod_stats = EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr;
-    store_wave_tile<EPI, OUT8>(smem + wid * 16384, aux, acc, wm, wn, m0, n0, lane, residual, nullptr, 1, C, ldc, M, N,
-                               prod_stats, M, o8);
+    if (OUT8 && C == nullptr)   // fp8-only output (FC1): 16-B element stores, gathered scale words
+        store_wave_tile_q8<EPI>(smem + wid * 16384, aux, acc, wm, wn, m0, n0, lane, M, N, o8);
+    else
+        store_wave_tile<EPI, OUT8>(smem + wid * 16384, aux, acc, wm, wn, m0, n0, lane, residual, nullptr, 1, C, ldc,
+                                   M, N, prod_stats, M, o8);
 }
 
 // MX quantisation of bf16 rows: one lane per 8 values, a DPP quad per 32-value block (gemm_common.h).
