@@ -149,6 +149,10 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
         }
     }
     constexpr bool PROD = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH);
+    // OUT8 with output row = m (every epilogue but PATCH): the wave owns whole scale words (two 64-row bricks x
+    // two K-blocks), gathered after the loop instead of one byte store per row and block
+    constexpr bool GATHER8 = OUT8 && EPI != VPF_EPI_PATCH;
+    uint32_t e8s[16];
     __builtin_amdgcn_wave_barrier();   // the image is private to this wave: LDS ops of one wave stay in order
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
@@ -209,12 +213,33 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
             // whole quads are in or out of range together (rows: a quad is one row; columns: N % 128 == 0)
             uint32_t e8;
             const uint2 q = mx8_quant8(v, e8);
+            e8s[it] = e8;
             if (ok) {
                 *reinterpret_cast<uint2*>(o8.q + orow * o8.ldq + n) = q;
-                if ((c16 & 3) == 0) o8.s[mx8_scale_byte(orow, n, o8.lds)] = (uint8_t)e8;
+                if (!GATHER8 && (c16 & 3) == 0) o8.s[mx8_scale_byte(orow, n, o8.lds)] = (uint8_t)e8;
             }
         }
         if (ok && C != nullptr) *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
+    }
+    if constexpr (GATHER8) {
+        // word w = brick (w >> 5), block (w >> 4) & 1, row r16 = w & 15; byte f = rows 16f + r16 of the brick;
+        // staged in bytes 64..127 of image rows 0..3 (the statistics partials use bytes 0..63)
+        __builtin_amdgcn_wave_barrier();
+        if ((c16 & 3) == 0) {
+#pragma unroll
+            for (int it = 0; it < 16; ++it) {
+                const int row = it * 8 + (lane >> 3);
+                const int w = (row >> 6) * 32 + (c16 >> 2) * 16 + (row & 15);
+                img[(w >> 4) * 128 + 64 + (w & 15) * 4 + ((row >> 4) & 3)] = (char)e8s[it];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t word = *reinterpret_cast<const uint32_t*>(img + (lane >> 4) * 128 + 64 + (lane & 15) * 4);
+        const int nb = n0 + wn * 64;
+        const int R = m0 + wm * 128 + (lane >> 5) * 64;   // brick row base
+        if (nb < N && R < o8.lds)
+            reinterpret_cast<uint32_t*>(o8.s)[(int64_t)(nb >> 7) * o8.lds + R + (((nb >> 5) & 3) + ((lane >> 4) & 1)) * 16 +
+                                              (lane & 15)] = word;
     }
     if constexpr (PROD) {
         const int nb = n0 + wn * 64;
