@@ -12,11 +12,26 @@ int vpf_check_out8(const uint8_t* C8, int64_t ld8, const uint32_t* Cs, int64_t l
 namespace vpf {
 namespace gemm {
 
-typedef short bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// LDS fragment reads as inline asm: with LDS-DMA writes of other ring slots in flight, hipcc's waitcnt pass
+// cannot prove the reads independent and drains vmcnt(0) before them (losing the lookahead); kernels that use
+// these wait for them themselves (s_waitcnt lgkmcnt(0) tied to the fragment registers).
+__device__ __forceinline__ i32x4 lds16(const char* p) {
+    i32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lptr_t)p));
+    return v;
+}
+__device__ __forceinline__ int lds4(const void* p) {
+    int v;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lptr_t)p));
+    return v;
+}
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BM = 256, BN = 256;
 constexpr int NTHREADS = 512;

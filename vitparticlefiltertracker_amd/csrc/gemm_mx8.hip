@@ -24,22 +24,6 @@ using namespace vpf;
 using namespace vpf::gemm;
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-
-// LDS fragment reads as inline asm: hipcc's waitcnt pass cannot tell these reads from the in-flight LDS-DMA
-// writes of the other buffer and would drain vmcnt(0) before them (losing the lookahead); the kernel waits
-// for them itself (lgkmcnt(0) tied to the fragment registers, below).
-__device__ __forceinline__ i32x4 lds16(const char* p) {
-    i32x4 v;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lptr_t)p));
-    return v;
-}
-__device__ __forceinline__ int lds4(const void* p) {
-    int v;
-    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lptr_t)p));
-    return v;
-}
-
 namespace {
 
 constexpr int BK = 128;                                // fp8 K values per K-tile (128 B per row)
