@@ -5,6 +5,9 @@ A CPU restatement of the per-frame tracking path pinned by /root/repo/SPEC.md:
 * `oracle.pf`  — ctypes binding of `pf_oracle.c` (Philox, predict, crop+im2col, estimate, exact
   integer systematic resample), bit-reproducible scalar C.
 * `oracle.vit` — pure PyTorch-CPU fp32 functional ViT (timm/HF pre-norm semantics).
+* `oracle.mx8` — numpy MX-fp8 format (e4m3fn round-half-even encoding, block exponents, scale planes,
+  float64 GEMM on dequantised operands) for the fp8 path (configs[4]); pinned by the OCP value table and
+  torch's float8_e4m3fn cast (tests/test_oracle_mx8.py).
 * `oracle.tracker` — `OracleTracker`, the CPU mirror of `Tracker` used for end-to-end parity and as
   bench.py's `cpu_baseline` ("port" kind: the reference has no runnable code, README.md:1-63).
 

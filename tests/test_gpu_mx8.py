@@ -1,13 +1,14 @@
 """GPU (MI355X): the MX-fp8 path (BASELINE.json configs[4]) — quantiser, block-scaled GEMM
 and the fp8 copies written by GEMM epilogues — through the product ops / C-ABI.
 
-References: quantisation is bit-exact against a torch restatement of the rule in include/vpf.h ("MX8 operands":
-smallest block exponent with amax * 2^-E <= 448, RNE to e4m3fn via torch's own float8_e4m3fn cast on the CPU);
+References: quantisation is bit-exact against the CPU oracle oracle/mx8.py (the rule in include/vpf.h "MX8
+operands": smallest block exponent with amax * 2^-E <= 448, RNE to e4m3fn; pinned by tests/test_oracle_mx8.py);
 GEMMs against float64 products of the dequantised operands (so the tolerance covers only fp32 accumulation order
 and the final bf16 rounding); every fp8 copy written by an epilogue must equal vpf_quantize_mx8 of the bf16
 values the same epilogue stored, bit for bit."""
 import math
 
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as Fn
@@ -38,17 +39,12 @@ def E():
 
 
 def ref_quant(x: torch.Tensor):
-    """CPU restatement of the MX8 rule: (uint8[rows][K] codes, int32[rows][K/32] scale bytes)."""
-    x = x.cpu()
-    rows, K = x.shape
-    bits = (x.view(torch.int16).to(torch.int32) & 0x7FFF).view(rows, K // 32, 32)
-    am = bits.amax(-1)
-    be = am >> 7
-    ex = torch.where(be > 0, be - 127, torch.full_like(be, -126))
-    Ex = (ex - 8 + ((am & 0x7F) > 0x60).to(torch.int32)).clamp(-127, 125)
-    inv = torch.exp2(-Ex.to(torch.float32))
-    y = (x.float().view(rows, K // 32, 32) * inv[..., None]).view(rows, K)
-    return y.to(torch.float8_e4m3fn).view(torch.uint8), (Ex + 127).to(torch.int32)
+    """The oracle's MX8 rule (oracle/mx8.py, pinned by tests/test_oracle_mx8.py): (uint8[rows][K] codes,
+    int32[rows][K/32] scale bytes)."""
+    from oracle import mx8 as omx8
+    bits = x.contiguous().cpu().view(torch.int16).numpy().view(np.uint16)
+    codes, sc = omx8.quantize(bits)
+    return torch.from_numpy(codes), torch.from_numpy(sc.astype(np.int32))
 
 
 def quant(x: torch.Tensor):
