@@ -54,8 +54,23 @@ def pmc_traffic(arch_name: str, n_local: int, kernel: str):
         return None, "no PMC summary"
 
 
+# BASELINE.json configs as presets (global particle count, arch, dtype, frame). configs[0] is the reference's
+# CPU-runnable plumbing case (its CPU path is oracle/, timed as cpu_baseline); on the GPU it is ViT-Ti.
+PRESETS = {
+    0: dict(particles=256, arch="vit_tiny_patch16_224", dtype="bf16", frame="224x224"),
+    1: dict(particles=4096, arch="vit_base_patch16_224", dtype="bf16", frame="224x224"),
+    2: dict(particles=16384, arch="vit_base_patch16_224", dtype="bf16", frame="224x224"),
+    3: dict(particles=4096, arch="vit_large_patch14_336", dtype="bf16", frame="224x224"),
+    4: dict(particles=65536, arch="vit_base_patch16_224", dtype="fp8", frame="1080x1920"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", type=int, choices=sorted(PRESETS), default=None,
+                    help="BASELINE.json configs[i] (sets --particles/--arch/--dtype/--frame; the metric's own "
+                         "workload is configs[1], the default). configs[2]/[4] are 8-GPU sizes: with fewer ranks "
+                         "use --particles for the per-GPU share")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -68,7 +83,13 @@ def parse():
     ap.add_argument("--kernel-frames", type=int, default=2, help="eager frames timed per kernel (roofline)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (s); 0 = skip")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity cores)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.preset is not None:
+        given = {a.lstrip("-").split("=")[0].replace("-", "_") for a in sys.argv[1:] if a.startswith("--")}
+        for k, v in PRESETS[args.preset].items():
+            if k not in given:          # explicit flags win over the preset
+                setattr(args, k, v)
+    return args
 
 
 def cpu_baseline(arch_name: str, P: int, budget_s: float, threads: int):
