@@ -18,12 +18,15 @@ def main(argv=None) -> int:
     ap.add_argument("--config", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "config.yaml"))
     ap.add_argument("--frames", type=int, default=None, help="override input.frames")
     ap.add_argument("--out", default=None, help="write positions as JSON here")
+    ap.add_argument("--video-out", default=None,
+                    help="write the frames with the tracked box drawn: a .y4m file, or a directory of .ppm frames")
     args = ap.parse_args(argv)
 
     import torch
     import torch.distributed as dist
     from vitparticlefiltertracker_amd import Tracker, load_config
-    from vitparticlefiltertracker_amd.frames import iter_frames, prefetch, synthetic_clip
+    from vitparticlefiltertracker_amd.frames import (Y4MWriter, draw_box, iter_frames, prefetch, synthetic_clip,
+                                                      write_ppm)
 
     cfg = load_config(args.config)
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
@@ -37,14 +40,35 @@ def main(argv=None) -> int:
         src = itertools.islice(iter_frames(inp["source"]), n)
     frames = prefetch(src, depth=2)   # decode + pin on a host thread, overlapped with the GPU frame loop
     tr = Tracker(cfg)
-    tr.init(next(frames), inp["bbox0"])
+    first = next(frames)
+    tr.init(first, inp["bbox0"])
+    sink = None
+    if args.video_out and tr.rank == 0:
+        if args.video_out.lower().endswith(".y4m"):
+            sink = Y4MWriter(args.video_out)
+        else:
+            os.makedirs(args.video_out, exist_ok=True)
+
+    def emit(k, rgb, box):
+        if not args.video_out or tr.rank != 0:
+            return
+        img = draw_box(rgb.numpy() if hasattr(rgb, "numpy") else rgb, box)
+        if sink is not None:
+            sink.write(img)
+        else:
+            write_ppm(os.path.join(args.video_out, f"frame_{k:05d}.ppm"), img)
+
+    emit(0, first, inp["bbox0"])
     t0 = time.perf_counter()
     out = []
     for k, f in enumerate(frames, start=1):
         x, y, s = tr.track(f)
         out.append({"frame": k, "x": x, "y": y, "scale": s})
+        emit(k, f, tr.box((x, y, s)))
         if tr.rank == 0:
             print(f"frame {k:4d}  x={x:8.2f}  y={y:8.2f}  scale={s:6.3f}", flush=True)
+    if sink is not None:
+        sink.close()
     dt = time.perf_counter() - t0
     if tr.rank == 0:
         print(f"{len(out)} frames in {dt:.3f} s ({len(out) / max(dt, 1e-9):.2f} frames/s)", file=sys.stderr)

@@ -117,3 +117,28 @@ def test_prefetch_early_close():
     it = fr.prefetch(iter(_clip(50)), depth=1, pin=False)
     next(it)
     it.close()
+
+
+def test_draw_box_outline_and_clipping():
+    img = np.zeros((20, 30, 3), np.uint8)
+    out = fr.draw_box(img, (5, 4, 10, 8), color=(9, 8, 7), thickness=2)
+    assert img.sum() == 0                                     # input untouched
+    on = (out == np.array([9, 8, 7], np.uint8)).all(axis=2)
+    assert on[4, 5] and on[4, 14] and on[11, 5] and on[11, 14] and on[5, 6]   # corners and the 2-px border
+    assert not on[7, 8] and not on[3, 5] and not on[12, 5]   # interior and outside stay black
+    clipped = fr.draw_box(img, (-5, -5, 12, 12), thickness=1)   # partly outside: clipped, no error
+    assert clipped[6, 0:7].any() and clipped.shape == img.shape
+
+
+def test_y4m_writer_streams(tmp_path):
+    clip = _clip(4, 10, 12)
+    p = tmp_path / "w.y4m"
+    with fr.Y4MWriter(p) as w:
+        for f in clip:
+            w.write(f)
+    back = list(fr.read_y4m(p))
+    assert len(back) == 4 and np.abs(back[2].astype(int) - clip[2]).max() <= 3
+    with pytest.raises(ValueError, match="size"):
+        with fr.Y4MWriter(tmp_path / "x.y4m") as w:
+            w.write(clip[0])
+            w.write(clip[0][:5])

@@ -163,3 +163,47 @@ def test_main_reads_y4m_clip(tmp_path):
     for r in res:
         bx, by, bw, bh = target_box(r["frame"])
         assert abs(r["x"] - (bx + bw / 2)) < 16 and abs(r["y"] - (by + bh / 2)) < 16, r
+
+
+def test_template_update():
+    """likelihood.template_update = alpha: the template moves toward the feature at the estimate and stays unit;
+    alpha = 0 leaves it bit-identical."""
+    from vitparticlefiltertracker_amd import Tracker
+    clip = synthetic_clip(4)
+    outs = {}
+    for alpha in (0.0, 0.5):
+        cfg = load_config({"model": {"arch": "vit_tiny_patch16_224", "dtype": "bf16"},
+                           "particles": {"num": 128, "seed": 3}, "likelihood": {"template_update": alpha}})
+        tr = Tracker(cfg)
+        tr.init(clip[0], (80, 80, 64, 64))
+        t0 = tr.template.clone()
+        est = [tr.track(f) for f in clip[1:]]
+        outs[alpha] = (t0, tr.template.clone(), est)
+    t0, t1, _ = outs[0.0]
+    assert torch.equal(t0, t1)
+    t0, t1, est = outs[0.5]
+    assert not torch.equal(t0, t1)
+    assert abs(t1.norm().item() - 1.0) < 1e-5
+    cos = torch.dot(t0, t1).item()
+    assert 0.5 < cos < 1.0, cos
+    for k, (x, y, s) in enumerate(est, start=1):     # still on the target
+        assert abs(x - (80 + 2 * k + 32)) < 16 and abs(y - (80 + k + 32)) < 16
+
+
+def test_main_video_out(tmp_path):
+    """main.py --video-out writes every frame with the tracked box overlaid (a .y4m sink)."""
+    import sys
+    import yaml
+    from vitparticlefiltertracker_amd.frames import read_y4m
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+    import main as vpf_main
+    cfg = {"model": {"arch": "vit_tiny_patch16_224", "dtype": "bf16"}, "particles": {"num": 128, "seed": 3},
+           "input": {"source": "synthetic", "frames": 4}}
+    cpath = tmp_path / "config.yaml"
+    cpath.write_text(yaml.safe_dump(cfg))
+    vid = tmp_path / "out.y4m"
+    assert vpf_main.main(["--config", str(cpath), "--video-out", str(vid)]) == 0
+    frames = list(read_y4m(vid))
+    assert len(frames) == 4 and frames[0].shape == (224, 224, 3)
+    red = (frames[2][..., 0] > 200) & (frames[2][..., 1] < 60) & (frames[2][..., 2] < 60)
+    assert red.sum() > 100                          # the box outline is there

@@ -104,3 +104,14 @@ def test_ops_refuse_cpu_tensors():
     p = torch.zeros(3, 4)
     with pytest.raises(Exception):
         torch.ops.vpf.predict_(p, 0, 1, 1, [1.0, 1.0, 0.1], 10.0, 10.0, [0.5, 2.0])
+
+
+def test_config_template_update_range():
+    from vitparticlefiltertracker_amd.config import load_config
+    assert load_config(None)["likelihood"]["template_update"] == 0.0
+    assert load_config({"likelihood": {"template_update": 0.25}})["likelihood"]["template_update"] == 0.25
+    with pytest.raises(ValueError, match="template_update"):
+        load_config({"likelihood": {"template_update": 1.5}})
+    assert load_config({"model": {"dtype": "fp8"}})["model"]["dtype"] == "fp8"
+    with pytest.raises(ValueError, match="dtype"):
+        load_config({"model": {"dtype": "int4"}})

@@ -81,7 +81,8 @@ DEFAULTS: Dict[str, Any] = {
         "scale_range": [0.5, 2.0],
         "seed": 1234,
     },
-    "likelihood": {"lambda": 20.0, "weight_bits": 40},
+    "likelihood": {"lambda": 20.0, "weight_bits": 40,
+                   "template_update": 0.0},     # alpha: t <- normalise((1 - alpha) t + alpha f(estimate)); 0 = fixed
     "resample": {"method": "systematic"},
     "input": {"source": "synthetic", "frames": 32, "height": 224, "width": 224,
               "bbox0": [80, 80, 64, 64], "seed": 7},
@@ -116,6 +117,8 @@ def load_config(cfg: Optional[Any] = None) -> Dict[str, Any]:
         raise ValueError(f"unknown model.arch {arch!r}; known: {sorted(ARCHS)}")
     if out["model"]["dtype"] not in ("bf16", "fp8", "fp32"):
         raise ValueError("model.dtype must be 'bf16', 'fp8' or 'fp32'")
+    if not 0.0 <= float(out["likelihood"]["template_update"]) <= 1.0:
+        raise ValueError("likelihood.template_update must be in [0, 1]")
     if out["resample"]["method"] != "systematic":
         raise ValueError("only resample.method == 'systematic' is defined (SPEC S7)")
     return out

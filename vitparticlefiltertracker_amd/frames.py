@@ -148,25 +148,69 @@ def read_y4m(path, matrix: Optional[str] = None, full_range: Optional[bool] = No
             yield yuv_to_rgb(y, cb, cr, matrix, full_range)
 
 
+class Y4MWriter:
+    """Streaming YUV4MPEG2 writer (C444, or C420jpeg by 2x2 averaging): the output sink of main.py --video-out."""
+
+    def __init__(self, path, fps: int = 30, chroma: str = "444", matrix: str = "bt601", full_range: bool = False):
+        self.path, self.fps, self.matrix, self.full_range = path, fps, matrix, full_range
+        self.tag = "444" if chroma == "444" else "420jpeg"
+        self.fh = None
+        self.shape = None
+
+    def write(self, rgb: np.ndarray) -> None:
+        H, W = rgb.shape[:2]
+        if self.fh is None:
+            self.shape = (H, W)
+            extra = " XCOLORRANGE=FULL" if self.full_range else ""
+            self.fh = open(self.path, "wb")
+            self.fh.write(f"YUV4MPEG2 W{W} H{H} F{self.fps}:1 Ip A1:1 C{self.tag}{extra}\n".encode("ascii"))
+        elif (H, W) != self.shape:
+            raise ValueError("Y4MWriter: every frame must have the first frame's size")
+        y, u, v = rgb_to_yuv(rgb, self.matrix, self.full_range)
+        if self.tag != "444":
+            def sub(p):
+                pe = np.pad(p.astype(np.float32), ((0, H % 2), (0, W % 2)), mode="edge")
+                s = pe.reshape(pe.shape[0] // 2, 2, pe.shape[1] // 2, 2).mean((1, 3))
+                return np.clip(np.rint(s), 0, 255).astype(np.uint8)
+            u, v = sub(u), sub(v)
+        self.fh.write(b"FRAME\n")
+        self.fh.write(y.tobytes() + u.tobytes() + v.tobytes())
+
+    def close(self) -> None:
+        if self.fh is not None:
+            self.fh.close()
+            self.fh = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 def write_y4m(path, frames: Iterable[np.ndarray], fps: int = 30, chroma: str = "444", matrix: str = "bt601",
               full_range: bool = False) -> None:
     """Write RGB frames as YUV4MPEG2 (C444, or C420jpeg by 2x2 averaging) — fixtures and round-trip tests."""
-    frames = list(frames)
-    H, W = frames[0].shape[:2]
-    tag = "444" if chroma == "444" else "420jpeg"
-    extra = " XCOLORRANGE=FULL" if full_range else ""
-    with open(path, "wb") as fh:
-        fh.write(f"YUV4MPEG2 W{W} H{H} F{fps}:1 Ip A1:1 C{tag}{extra}\n".encode("ascii"))
+    with Y4MWriter(path, fps, chroma, matrix, full_range) as w:
         for f in frames:
-            y, u, v = rgb_to_yuv(f, matrix, full_range)
-            if tag != "444":
-                def sub(p):
-                    pe = np.pad(p.astype(np.float32), ((0, H % 2), (0, W % 2)), mode="edge")
-                    s = pe.reshape(pe.shape[0] // 2, 2, pe.shape[1] // 2, 2).mean((1, 3))
-                    return np.clip(np.rint(s), 0, 255).astype(np.uint8)
-                u, v = sub(u), sub(v)
-            fh.write(b"FRAME\n")
-            fh.write(y.tobytes() + u.tobytes() + v.tobytes())
+            w.write(f)
+
+
+def draw_box(rgb: np.ndarray, box, color=(255, 0, 0), thickness: int = 2) -> np.ndarray:
+    """A copy of the uint8 RGB frame with the (x, y, w, h) box outline drawn (clipped to the frame): the tracked
+    position overlay of main.py --video-out."""
+    out = np.array(rgb, dtype=np.uint8, copy=True)
+    H, W = out.shape[:2]
+    x0, y0 = int(round(box[0])), int(round(box[1]))
+    x1, y1 = int(round(box[0] + box[2])) - 1, int(round(box[1] + box[3])) - 1
+    t = max(1, int(thickness))
+    col = np.asarray(color, dtype=np.uint8)
+    for (ya, yb, xa, xb) in ((y0, y0 + t, x0, x1 + 1), (y1 - t + 1, y1 + 1, x0, x1 + 1),
+                             (y0, y1 + 1, x0, x0 + t), (y0, y1 + 1, x1 - t + 1, x1 + 1)):
+        ya, yb, xa, xb = max(ya, 0), min(yb, H), max(xa, 0), min(xb, W)
+        if ya < yb and xa < xb:
+            out[ya:yb, xa:xb] = col
+    return out
 
 
 # ---------------------------------------------------------------------------------------------- PPM / PGM

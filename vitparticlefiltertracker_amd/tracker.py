@@ -58,6 +58,7 @@ class Tracker:
                                 c["model"]["mean"], c["model"]["std"])
         self.lam = float(c["likelihood"]["lambda"])
         self.bits = int(c["likelihood"]["weight_bits"])
+        self.template_alpha = float(c["likelihood"]["template_update"])
         self.use_graph = bool(use_graph)
         self.pf: Optional[ParticleFilter] = None
         self.template: Optional[torch.Tensor] = None
@@ -151,8 +152,26 @@ class Tracker:
         self.pf.predict(self.frame_index)
         self.weigh()
         est = self.pf.estimate()
+        if self.template_alpha > 0.0:
+            self.update_template(est)
         self.pf.resample()
         return est
+
+    def update_template(self, state, alpha: Optional[float] = None) -> None:
+        """Template update: t <- normalise((1 - alpha) t + alpha f / |f|) with f the CLS
+        feature of the crop at `state` = (x, y, scale) of the current frame. In place, so the captured graph
+        keeps reading the same buffer; every rank computes the same bits (same estimate, same kernels)."""
+        a = self.template_alpha if alpha is None else float(alpha)
+        st = torch.tensor([[state[0]], [state[1]], [state[2]]], dtype=torch.float32, device=self.device)
+        f = self.engine.features(self._frame_dev, st, self.box_wh)[0]
+        t = (1.0 - a) * self.template + a * (f / f.norm())
+        self.template.copy_(t / t.norm())
+
+    def box(self, state) -> Tuple[float, float, float, float]:
+        """(x, y, w, h) of the box a state (centre x, y, scale) stands for (SPEC S3: scale x template size)."""
+        x, y, s = (float(v) for v in state)
+        w, h = s * self.box_wh[0], s * self.box_wh[1]
+        return x - 0.5 * w, y - 0.5 * h, w, h
 
     def run(self, frames: Iterable) -> np.ndarray:
         return np.array([self.track(f) for f in frames], dtype=np.float64)
