@@ -207,3 +207,48 @@ def test_main_video_out(tmp_path):
     assert len(frames) == 4 and frames[0].shape == (224, 224, 3)
     red = (frames[2][..., 0] > 200) & (frames[2][..., 1] < 60) & (frames[2][..., 2] < 60)
     assert red.sum() > 100                          # the box outline is there
+
+
+def test_multitracker_one_target_equals_tracker():
+    """MultiTracker's batched pass is row-independent: with one target it reproduces Tracker bit for bit."""
+    from vitparticlefiltertracker_amd import MultiTracker, Tracker
+    cfg = _tiny_cfg(128, "bf16")
+    w = make_vit_weights(ARCHS["vit_tiny_patch16_224"], seed=3)
+    clip = synthetic_clip(5)
+    tr = Tracker(cfg, weights=w)
+    tr.init(clip[0], (80, 80, 64, 64))
+    mt = MultiTracker(cfg, 1, weights=w)
+    mt.init(clip[0], [(80, 80, 64, 64)])
+    for f in clip[1:]:
+        a = tr.track(f)
+        (b,) = mt.track(f)
+        assert a == b
+    assert torch.equal(tr.pf.particles, mt.pfs[0].particles)
+
+
+def test_multitracker_two_targets():
+    """Two textured targets with their own box sizes and trajectories, tracked in one batched ViT pass."""
+    from vitparticlefiltertracker_amd import MultiTracker
+    rng = np.random.default_rng(11)
+    bg = rng.integers(0, 256, (240, 320, 3), dtype=np.uint8)
+    tex = [np.random.default_rng(s).integers(0, 256, (h, w, 3), dtype=np.uint8) for s, (w, h) in
+           ((21, (48, 48)), (22, (64, 40)))]
+    starts, vel = [(40, 50), (200, 150)], [(3, 1), (-2, -2)]
+    clip = []
+    for t in range(6):
+        f = bg.copy()
+        for k in range(2):
+            x, y = starts[k][0] + vel[k][0] * t, starts[k][1] + vel[k][1] * t
+            h, w = tex[k].shape[:2]
+            f[y:y + h, x:x + w] = tex[k]
+        clip.append(f)
+    cfg = load_config({"model": {"arch": "vit_tiny_patch16_224", "dtype": "bf16"},
+                       "particles": {"num": 256, "seed": 7}})
+    mt = MultiTracker(cfg, 2)
+    mt.init(clip[0], [(40, 50, 48, 48), (200, 150, 64, 40)])
+    for t, f in enumerate(clip[1:], start=1):
+        est = mt.track(f)
+        for k, (x, y, s) in enumerate(est):
+            h, w = tex[k].shape[:2]
+            cx, cy = starts[k][0] + vel[k][0] * t + w / 2, starts[k][1] + vel[k][1] * t + h / 2
+            assert abs(x - cx) < 16 and abs(y - cy) < 16, (t, k, x, y, cx, cy)

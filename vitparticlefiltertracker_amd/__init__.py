@@ -3,6 +3,7 @@ tugitbartlomiej/ViTParticleFilterTracker; see SPEC.md).
 
 Public API (the names the reference's main.py would use):
   Tracker(cfg).init(frame, bbox); Tracker.track(frame) -> (x, y, scale)
+  MultiTracker(cfg, n_objects).init(frame, bboxes); .track(frame) -> [(x, y, scale)] (one batched ViT pass)
   ParticleFilter(...).predict() / .update(features, template) / .estimate() / .resample()
   load_config(path | dict | None)
 The compute runs in libvpf.so (hand-written gfx950 HIP kernels) through torch.ops.vpf.* custom ops; there
@@ -18,6 +19,9 @@ def __getattr__(name):
     if name == "Tracker":
         from .tracker import Tracker
         return Tracker
+    if name == "MultiTracker":
+        from .tracker import MultiTracker
+        return MultiTracker
     if name == "ParticleFilter":
         from .particle_filter import ParticleFilter
         return ParticleFilter

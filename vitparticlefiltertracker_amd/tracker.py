@@ -14,7 +14,7 @@ Per frame: predict (eager launch; its frame index is a kernel argument) -> [HIP 
 from __future__ import annotations
 
 import os
-from typing import Iterable, Optional, Tuple
+from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -175,3 +175,102 @@ class Tracker:
 
     def run(self, frames: Iterable) -> np.ndarray:
         return np.array([self.track(f) for f in frames], dtype=np.float64)
+
+
+class MultiTracker:
+    """Several targets in one frame loop: one ParticleFilter per target, and ONE batched
+    ViT forward over every target's particles per frame (crops with each target's own template box, one patch
+    GEMM / encoder / final LN over all K*P crops, cosine weights against each target's own template), captured
+    into one HIP graph. Target k's particle stream is seeded with particles.seed + k, so a MultiTracker with one
+    target reproduces Tracker bit for bit. Single GPU (world size 1)."""
+
+    def __init__(self, cfg=None, n_objects: int = 1, device=None, use_graph: bool = True, weights=None):
+        self.cfg = load_config(cfg)
+        if not torch.cuda.is_available():
+            raise _lib.VPFError("MultiTracker runs on the HIP device only")
+        if n_objects < 1:
+            raise ValueError("n_objects >= 1")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        torch.cuda.set_device(self.device)
+        c = self.cfg
+        self.arch = arch_of(c)
+        self.K = int(n_objects)
+        self.P = int(c["particles"]["num"])
+        w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
+        self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, self.K * self.P, c["model"]["mean"],
+                                c["model"]["std"])
+        self.lam = float(c["likelihood"]["lambda"])
+        self.bits = int(c["likelihood"]["weight_bits"])
+        self.use_graph = bool(use_graph)
+        self.pfs: List[ParticleFilter] = []
+        self.templates: List[torch.Tensor] = []
+        self.boxes: List[Tuple[float, float]] = []
+        self._frame_dev: Optional[torch.Tensor] = None
+        self._graph = None
+        self.frame_index = 0
+
+    def _upload(self, frame) -> torch.Tensor:
+        arr = torch.as_tensor(np.ascontiguousarray(frame.cpu().numpy() if isinstance(frame, torch.Tensor) else frame,
+                                                   dtype=np.uint8))
+        if self._frame_dev is None or tuple(self._frame_dev.shape) != tuple(arr.shape):
+            self._frame_dev = torch.empty(arr.shape, dtype=torch.uint8, device=self.device)
+            self._graph = None
+        self._frame_dev.copy_(arr)
+        return self._frame_dev
+
+    def init(self, frame, bboxes: Sequence) -> None:
+        if len(bboxes) != self.K:
+            raise ValueError(f"expected {self.K} boxes")
+        fd = self._upload(frame)
+        c = self.cfg
+        self.pfs, self.templates, self.boxes = [], [], []
+        for k, (bx, by, bw, bh) in enumerate(bboxes):
+            bx, by, bw, bh = float(bx), float(by), float(bw), float(bh)
+            cx, cy = bx + 0.5 * bw, by + 0.5 * bh
+            one = torch.tensor([[cx], [cy], [1.0]], dtype=torch.float32, device=self.device)
+            f = self.engine.features(fd, one, (bw, bh))[0].clone()
+            self.templates.append((f / f.norm()).contiguous())
+            self.boxes.append((bw, bh))
+            self.pfs.append(ParticleFilter(self.P, (cx, cy, 1.0), c["particles"]["motion_std"],
+                                           c["particles"]["scale_range"], int(c["particles"]["seed"]) + k,
+                                           self.device, (fd.shape[0], fd.shape[1]), self.lam, self.bits))
+        self._graph = None
+        self.frame_index = 0
+
+    def _forward(self) -> None:
+        eng = self.engine
+        n = eng.embed_many(self._frame_dev, [pf.particles for pf in self.pfs], self.boxes)
+        eng.encoder(n)
+        for k in range(self.K):
+            eng.weights_from_tokens(self.P, self.templates[k], self.lam, self.bits, row0=k * self.P)
+
+    def _capture(self) -> None:
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._forward()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._forward()
+        self._graph = g
+
+    def track(self, frame) -> List[Tuple[float, float, float]]:
+        if not self.pfs:
+            raise RuntimeError("call init(frame, bboxes) first")
+        self._upload(frame)
+        self.frame_index += 1
+        for pf in self.pfs:
+            pf.predict(self.frame_index)
+        if self.use_graph:
+            if self._graph is None:
+                self._capture()
+            self._graph.replay()
+        else:
+            self._forward()
+        out = []
+        for k, pf in enumerate(self.pfs):
+            pf.set_weights(self.engine.Q[k * self.P:(k + 1) * self.P])
+            out.append(pf.estimate())
+            pf.resample()
+        return out

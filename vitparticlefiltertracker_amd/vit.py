@@ -205,6 +205,13 @@ class ViTEngine:
             self._rgba_hw = hw
         _run(T, "crop_patches", vpf.crop_patches, frame, self.rgba, particles, [float(box_wh[0]), float(box_wh[1])],
              A.img_size, A.patch, self.norm_ab, patches)
+        self._embed_rest(n)
+
+    def _embed_rest(self, n: int) -> None:
+        """Patch GEMM (+ bias + position rows, CLS-offset token rows) and the CLS rows for the first n crops."""
+        A = self.arch
+        T = self.timer
+        patches = self.patches[: n * A.n_patches]
         h = self.h[:n]
         pl = self.planes(n) if self.use_planes else None
         if self.fp8:
@@ -223,6 +230,25 @@ class ViTEngine:
             _run(T, "gemm_patch", vpf.gemm, patches, self.w_pe, self.b_pe, None, self.pos, A.n_patches, None, None,
                  _lib.VPF_EPI_PATCH, h)
             _run(T, "cls_rows", vpf.cls_rows_, h, self.cls, self.pos)
+
+    def embed_many(self, frame: torch.Tensor, particle_sets, boxes) -> int:
+        """Multi-object embed: particle set k (float32[3][n_k]) cropped with its own template box boxes[k] into
+        consecutive patch rows, then one patch GEMM + CLS rows over all of them. Returns the total count."""
+        A = self.arch
+        n = sum(int(p.shape[1]) for p in particle_sets)
+        assert n <= self.batch
+        hw = (int(frame.shape[0]), int(frame.shape[1]))
+        if getattr(self, "_rgba_hw", None) != hw:
+            self.rgba = ops.rgba_workspace(hw, frame.device)
+            self._rgba_hw = hw
+        row = 0
+        for parts, box in zip(particle_sets, boxes):
+            k = int(parts.shape[1])
+            _run(self.timer, "crop_patches", vpf.crop_patches, frame, self.rgba, parts, [float(box[0]), float(box[1])],
+                 A.img_size, A.patch, self.norm_ab, self.patches[row * A.n_patches:(row + k) * A.n_patches])
+            row += k
+        self._embed_rest(n)
+        return n
 
     def planes(self, n: int) -> torch.Tensor:
         """Statistics planes of h[:n] (plane stride n*N rows, as the producing GEMMs write them)."""
@@ -346,10 +372,12 @@ class ViTEngine:
                 _run(T, "gemm_fc1" + tag, vpf.gemm, xx, L["wfc1"], L["bfc1"], None, None, 0, None, None, GELU, hd_)
                 _run(T, "gemm_fc2" + tag, vpf.gemm, hd_, L["wfc2"], L["bfc2"], hh, None, 0, None, None, RES, hh)
 
-    def weights_from_tokens(self, n: int, tmpl: torch.Tensor, lam: float, bits: int, want_feat: bool = False):
-        _run(self.timer, "cls_weight", vpf.cls_weight, self.h[:n], self.ng, self.nb, self.arch.ln_eps, tmpl,
-             float(lam), int(bits), self.Q[:n], self.feat[:n] if want_feat else None, self.sim[:n])
-        return self.Q[:n]
+    def weights_from_tokens(self, n: int, tmpl: torch.Tensor, lam: float, bits: int, want_feat: bool = False,
+                            row0: int = 0):
+        r = slice(row0, row0 + n)
+        _run(self.timer, "cls_weight", vpf.cls_weight, self.h[r], self.ng, self.nb, self.arch.ln_eps, tmpl,
+             float(lam), int(bits), self.Q[r], self.feat[r] if want_feat else None, self.sim[r])
+        return self.Q[r]
 
     def features(self, frame: torch.Tensor, particles: torch.Tensor, box_wh) -> torch.Tensor:
         """LN'd CLS features [n][D] fp32 (template init, tests)."""
