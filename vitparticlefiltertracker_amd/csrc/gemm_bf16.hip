@@ -236,14 +236,23 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             *reinterpret_cast<float2*>(aux + 2048 + tid * 8) = make_float2(mean, __builtin_amdgcn_rsqf(var + ln_eps));
         }
     }
-    __syncthreads();   // every wave is done with the operand ring; reuse it as 8 x 16 KiB images
+    // no LDS-DMA is outstanding after the K loop; saying so with the builtin (which hipcc's waitcnt pass reads,
+    // unlike asm) keeps it from draining vmcnt(0) - and with it the residual loads - at the first LDS access below
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    uint4 res[16];
+    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
+    // every wave is done with the operand ring (reused as 8 x 16 KiB images) and the LN combine is visible; a
+    // raw barrier, so the residual loads stay in flight across it (no DMA is outstanding after the K loop)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     char* img = smem + wid * 16384;
     if constexpr (DEEP) {   // the four 32 KiB slots other than the aux slot
         const int region = (wid >> 1) + ((wid >> 1) >= (nk % 3) ? 1 : 0);
         img = smem + region * OPERAND_BYTES + (wid & 1) * 16384;
     }
     float* prod_stats = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) ? stats_out : nullptr;
-    store_wave_tile<EPI, OUT8>(img, aux, acc, wm, wn, m0, n0, lane, residual, pos, g2, C, ldc, M, N, prod_stats,
+    store_wave_tile<EPI, OUT8>(img, aux, acc, wm, wn, m0, n0, lane, res, pos, g2, C, ldc, M, N, prod_stats,
                                stats_rows, o8);
 }
 

@@ -145,24 +145,28 @@ __device__ __forceinline__ void epi_to_image(char* img, const char* aux, const f
     }
 }
 
+// The residual rows a lane adds in store_wave_tile (EPI_BIAS_RESIDUAL): 16 x 16 B, all in flight at once. The
+// kernels issue this right after their K loop, before the epilogue barrier (a raw s_barrier, so the loads stay
+// in flight across it), which gives them the LN combine, the barrier and the image writes to land under.
+__device__ __forceinline__ void load_residual(uint4 (&res)[16], const bf16_t* residual, int wm, int wn, int m0,
+                                              int n0, int lane, int ldc, int M, int N) {
+    const int c16 = lane & 7;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int m = m0 + wm * 128 + it * 8 + (lane >> 3);
+        const int n = n0 + wn * 64 + c16 * 8;
+        res[it] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(residual + (int64_t)m * ldc + n)
+                                   : make_uint4(0, 0, 0, 0);
+    }
+}
+
 template <int EPI, bool OUT8>
 __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
-                                                int m0, int n0, int lane, const bf16_t* residual,
+                                                int m0, int n0, int lane, const uint4 (&res)[16],
                                                 const float* __restrict__ pos, int g2, bf16_t* C, int ldc, int M,
                                                 int N, float* stats_out, int stats_rows, Out8 o8) {
     epi_to_image<EPI>(img, aux, acc, wm, wn, lane);
     const int c16 = lane & 7;
-    uint4 res[16];
-    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
-        // all 16 residual rows of this lane in flight at once, under the LDS round trip below
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int m = m0 + wm * 128 + it * 8 + (lane >> 3);
-            const int n = n0 + wn * 64 + c16 * 8;
-            res[it] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(residual + (int64_t)m * ldc + n)
-                                       : make_uint4(0, 0, 0, 0);
-        }
-    }
     constexpr bool PROD = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH);
     // OUT8 with output row = m (every epilogue but PATCH): the wave owns whole scale words (two 64-row bricks x
     // two K-blocks), gathered after the loop instead of one byte store per row and block

@@ -216,12 +216,19 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
             *reinterpret_cast<float2*>(aux + 2048 + tid * 8) = make_float2(mean, __builtin_amdgcn_rsqf(var + ln_eps));
         }
     }
-    __syncthreads();   // the ring is free: 8 x 16 KiB epilogue images
+    // no LDS-DMA is outstanding after the K loop; saying so with the builtin (which hipcc's waitcnt pass reads,
+    // unlike asm) keeps it from draining vmcnt(0) - and with it the residual loads - at the first LDS access below
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    uint4 res[16];
+    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // raw barrier: the residual loads stay in flight
+    __builtin_amdgcn_s_barrier();   // the ring is free: 8 x 16 KiB epilogue images
+    asm volatile("" ::: "memory");
     float* prod_stats = EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr;
     if (OUT8 && C == nullptr)   // fp8-only output (FC1): 16-B element stores, gathered scale words
         store_wave_tile_q8<EPI>(smem + wid * 16384, aux, acc, wm, wn, m0, n0, lane, M, N, o8);
     else
-        store_wave_tile<EPI, OUT8>(smem + wid * 16384, aux, acc, wm, wn, m0, n0, lane, residual, nullptr, 1, C, ldc,
+        store_wave_tile<EPI, OUT8>(smem + wid * 16384, aux, acc, wm, wn, m0, n0, lane, res, nullptr, 1, C, ldc,
                                    M, N, prod_stats, M, o8);
 }
 
