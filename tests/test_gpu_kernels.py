@@ -343,6 +343,66 @@ def test_attention_q_rows(dtype, B, N, H):
     assert torch.all(part2[:, 2:] == 5.0)
 
 
+@pytest.mark.parametrize("B,N,H", [(3, 197, 12), (5, 197, 6), (2, 256, 12), (4, 1, 6), (64, 50, 12)])
+def test_cls_attn_fold(B, N, H):
+    """The last block's CLS attention with K / V never formed (vpf_cls_attn_fold_bf16) against an fp64
+    restatement: LNraw from the statistics planes, s_hj = (LNraw_j . G_h + q_h . bk_h) / 8, U_h = sum_j p_hj
+    LNraw_j. Then the whole identity: W'_v,h U_h + b'_v equals the explicit softmax(q k^T / 8) v with
+    k, v = LN(h) W'^T + b' (tolerance: bf16 rounding of LNraw in the dots and of the output)."""
+    torch.manual_seed(B * N + H)
+    D = 64 * H
+    h = (torch.randn(B, N, D, device=DEV) * 1.3 + 0.2).to(torch.bfloat16)
+    planes = _planes_ref(h.view(B * N, D), H).float().contiguous()
+    Wk = torch.randn(D, D, device=DEV) / D ** 0.5
+    Wv = torch.randn(D, D, device=DEV) / D ** 0.5
+    bk = 0.3 * torch.randn(D, device=DEV)
+    bv = 0.3 * torch.randn(D, device=DEV)
+    qall = (torch.randn(B, 2, D, device=DEV) * 3.0).to(torch.bfloat16)   # scores of std ~3: a peaked softmax
+    q = qall[:, 0]                                        # row-strided view (row stride 2D), as in vit.py
+    qd = q.double().reshape(B, H, 64)
+    G = torch.einsum("bhd,hdi->bhi", qd, Wk.double().view(H, 64, D)).to(torch.bfloat16).contiguous()   # [B][H][D]
+    out = torch.full((B, H * D), float("nan"), device=DEV, dtype=torch.bfloat16)
+    vpf().cls_attn_fold_(h, planes, 1e-6, G.view(B, H * D), q, bk, H, out)
+    hd_ = h.double()
+    mean = hd_.mean(-1, keepdim=True)
+    var = (hd_ * hd_).mean(-1, keepdim=True) - mean * mean
+    ln = (hd_ - mean) / torch.sqrt(var + 1e-6)                                            # [B][N][D]
+    c0 = (qd * bk.double().view(H, 64)).sum(-1)                                           # [B][H]
+    s = (torch.einsum("bnd,bhd->bhn", ln, G.double()) + c0[..., None]) * 0.125
+    p = torch.softmax(s, -1)
+    U = torch.einsum("bhn,bnd->bhd", p, ln)
+    torch.testing.assert_close(out.double().view(B, H, D), U, rtol=2e-2, atol=1e-2 * U.abs().max().item())
+    # the algebra: W'_v,h U_h + b'_v == softmax(q k^T / 8) v on the explicit K, V
+    k = (ln @ Wk.double().t() + bk.double()).view(B, N, H, 64)
+    v = (ln @ Wv.double().t() + bv.double()).view(B, N, H, 64)
+    att = torch.softmax(torch.einsum("bhd,bnhd->bhn", qd, k) * 0.125, -1)
+    o_ref = torch.einsum("bhn,bnhd->bhd", att, v)
+    o = torch.einsum("bhi,hdi->bhd", out.double().view(B, H, D), Wv.double().view(H, 64, D)) + bv.double().view(H, 64)
+    torch.testing.assert_close(o, o_ref, rtol=3e-2, atol=2e-2 * o_ref.abs().max().item())
+
+
+def test_cls_attn_fold_argument_contract():
+    H, D, B, N = 12, 768, 2, 197
+    h = torch.zeros(B, N, D, device=DEV, dtype=torch.bfloat16)
+    planes = torch.zeros(H, B * N, 2, device=DEV)
+    G = torch.zeros(B, H * D, device=DEV, dtype=torch.bfloat16)
+    q = torch.zeros(B, D, device=DEV, dtype=torch.bfloat16)
+    bk = torch.zeros(D, device=DEV)
+    out = torch.empty(B, H * D, device=DEV, dtype=torch.bfloat16)
+    from vitparticlefiltertracker_amd._lib import VPFError
+    with pytest.raises((ValueError, VPFError)):
+        vpf().cls_attn_fold_(h, planes[:, :B * N - 1], 1e-6, G, q, bk, H, out)       # planes too short
+    h16 = torch.zeros(B, N, 1024, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises((ValueError, VPFError)):
+        vpf().cls_attn_fold_(h16, torch.zeros(16, B * N, 2, device=DEV), 1e-6, torch.zeros(B, 16 * 1024, device=DEV,
+                             dtype=torch.bfloat16), torch.zeros(B, 1024, device=DEV, dtype=torch.bfloat16),
+                             torch.zeros(1024, device=DEV), 16, torch.empty(B, 16 * 1024, device=DEV,
+                                                                            dtype=torch.bfloat16))   # H = 16
+    h300 = torch.zeros(1, 300, D, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises((ValueError, VPFError)):
+        vpf().cls_attn_fold_(h300, torch.zeros(H, 300, 2, device=DEV), 1e-6, G[:1], q[:1], bk, H, out[:1])  # N > 256
+
+
 @pytest.mark.parametrize("mode", ["0", "2"])
 @pytest.mark.parametrize("B,N,H", [(100, 197, 12), (90, 256, 12), (96, 280, 12)])
 def test_attention_bf16_large(B, N, H, mode, monkeypatch):

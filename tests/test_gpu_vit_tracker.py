@@ -51,6 +51,31 @@ def test_vit_features_vs_oracle(name, dtype, n):
         assert cos.min().item() > (0.999 if dtype == "bf16" else 0.99), cos
 
 
+@pytest.mark.parametrize("name,dtype", [("vit_base_patch16_224", "bf16"), ("vit_small_patch16_224", "fp8")])
+def test_cls_fused_tail_equals_kv_path(name, dtype, monkeypatch):
+    """The last block's CLS attention without K / V (vpf_cls_attn_fold_bf16 between two block-diagonal GEMMs)
+    against the K / V GEMM + attention path it replaces (VPF_CLS_FUSED=0), and both against the fp32 oracle."""
+    from vitparticlefiltertracker_amd.vit import ViTEngine
+    arch = ARCHS[name]
+    w = make_vit_weights(arch, seed=6, perturb_affine=True)
+    n = 33
+    frame, p = _crops(arch, n, seed=2)
+    fd, pd = torch.from_numpy(frame).to(DEV), torch.from_numpy(p).to(DEV)
+    fused = ViTEngine(arch, w, dtype, DEV, n)
+    assert fused.cls_fused
+    f1 = fused.features(fd, pd, (64.0, 64.0)).double().cpu()
+    monkeypatch.setenv("VPF_CLS_FUSED", "0")
+    plain = ViTEngine(arch, w, dtype, DEV, n)
+    assert not plain.cls_fused
+    f0 = plain.features(fd, pd, (64.0, 64.0)).double().cpu()
+    cos = torch.nn.functional.cosine_similarity(f1, f0, dim=1)
+    assert cos.min().item() > 0.9995, cos
+    patches = pf.crop_patches(frame, p, (64.0, 64.0), arch.img_size, arch.patch, arch.patch_kp, (0.5,) * 3, (0.5,) * 3)
+    ref = ovit.features_from_patches(torch.from_numpy(patches), w, arch).double()
+    bar = 0.999 if dtype == "bf16" else 0.99
+    assert torch.nn.functional.cosine_similarity(f1, ref, dim=1).min().item() > bar
+
+
 def _tiny_cfg(P, dtype, arch="vit_tiny_patch16_224"):
     return load_config({"model": {"arch": arch, "dtype": dtype, "weights": {"seed": 3}},
                         "particles": {"num": P, "seed": 99}})

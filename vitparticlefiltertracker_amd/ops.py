@@ -361,6 +361,29 @@ def attention_q8_(qkv: torch.Tensor, heads: int, q8: torch.Tensor, s8: torch.Ten
          s8.shape[1], stream_ptr())
 
 
+@torch.library.custom_op("vpf::cls_attn_fold_", mutates_args={"out"}, device_types="cuda")
+def cls_attn_fold_(tokens: torch.Tensor, planes: torch.Tensor, eps: float, G: torch.Tensor, q: torch.Tensor,
+                   bk: torch.Tensor, heads: int, out: torch.Tensor) -> None:
+    """H6 for the last block's CLS query, K / V never formed (LN-folded bf16): tokens [n][N][D] with statistics
+    planes [D/64][n*N][2]; G [n][H*D] (W'_k,h^T q_h), q the CLS queries [n][D] (row-strided), bk = b'_k;
+    out [n][H*D] = per head sum_j p_hj LNraw_j (vpf_cls_attn_fold_bf16)."""
+    _dev(tokens, planes, G, bk, out)
+    _chk(q.is_cuda and tokens.dtype == _BF16 and G.dtype == _BF16 and q.dtype == _BF16 and out.dtype == _BF16,
+         "cls_attn_fold_: bf16 tokens / G / q / out")
+    n, N, D = tokens.shape
+    _chk(tokens.is_contiguous() and D == 64 * heads, "cls_attn_fold_: contiguous tokens, head dim 64")
+    _chk(planes.dtype == _F32 and planes.dim() == 3 and planes.shape[0] == heads and planes.shape[1] >= n * N
+         and planes.stride(2) == 1 and planes.stride(1) == 2, "cls_attn_fold_: planes f32[D/64][n*N][2]")
+    _chk(bk.dtype == _F32 and bk.numel() >= D and bk.is_contiguous(), "cls_attn_fold_: bk f32[D]")
+    rg, ldg = _rows(G, "cls_attn_fold_ G")
+    rq, ldq = _rows(q, "cls_attn_fold_ q")
+    ro, ldo = _rows(out, "cls_attn_fold_ out")
+    _chk(rg == n and rq == n and ro == n and G.shape[1] == heads * D and q.shape[1] == D and out.shape[1] == heads * D,
+         "cls_attn_fold_: shapes")
+    call("vpf_cls_attn_fold_bf16", ptr(tokens), n, N, heads, ptr(planes), planes.stride(0) // 2, eps, ptr(G), ldg,
+         ptr(q), ldq, ptr(bk), 64 ** -0.5, ptr(out), ldo, stream_ptr())
+
+
 @torch.library.custom_op("vpf::cls_weight", mutates_args={"Q", "feat", "sim"}, device_types="cuda")
 def cls_weight(tokens: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, tmpl: torch.Tensor,
                lam: float, bits: int, Q: torch.Tensor, feat: Optional[torch.Tensor],

@@ -28,6 +28,7 @@ for N > 256, the attention output and proj).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional
 
 import torch
@@ -161,6 +162,25 @@ class ViTEngine:
             self.layers.append(L)
         self.ng = f32(weights["norm.weight"])
         self.nb = f32(weights["norm.bias"])
+        # the last block's CLS attention without K / V (vpf_cls_attn_fold_bf16): LN-folded bf16 with statistics
+        # planes, head dim 64, 6 or 12 heads, N <= 256. Two block-diagonal weights carry the per-head algebra:
+        #   G[p][h D + i] = sum_{k in head h} q[p][k] W'_k[k][i]        (W_G[h D + i][k] = W'_k[k][i])
+        #   x[p][64 h + d] = sum_i W'_v[64 h + d][i] U[p][h D + i] + b'_v (W_V[64 h + d][h D + i] = W'_v[64 h + d][i])
+        # VPF_CLS_FUSED=0 keeps the K / V GEMM + attention path (A/B, tests).
+        H = A.heads
+        self.cls_fused = (self.fold_ln and H in (6, 12) and D == 64 * H and N <= 256
+                          and os.environ.get("VPF_CLS_FUSED", "1") != "0")
+        if self.cls_fused:
+            L = self.layers[-1]
+            Wk, Wv = L["wqkv"][D:2 * D].float(), L["wqkv"][2 * D:].float()
+            wg = torch.zeros(H * D, D, device=dev, dtype=torch.float32)
+            wv = torch.zeros(D, H * D, device=dev, dtype=torch.float32)
+            for h in range(H):
+                c = slice(64 * h, 64 * h + 64)
+                wg[h * D:(h + 1) * D, c] = Wk[c, :].t()
+                wv[c, h * D:(h + 1) * D] = Wv[c, :]
+            self.w_clsG, self.w_clsV = wg.to(dt).contiguous(), wv.to(dt).contiguous()
+            self.b_clsG = torch.zeros(H * D, device=dev, dtype=torch.float32)
         self._alloc(self.batch)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.timer: Optional[KernelTimer] = None
@@ -189,6 +209,9 @@ class ViTEngine:
             self.hid8 = ops.mx8_empty(n * N, F, dev)
         # the MX8 consumers read at most 13 statistics planes (LDS budget, vpf_gemm_mx8)
         self.planes8 = self.use_planes and self.parts <= 13
+        if self.cls_fused:
+            self.clsG = torch.empty(n, A.heads * D, device=dev, dtype=dt)
+            self.clsU = torch.empty(n, A.heads * D, device=dev, dtype=dt)
         self.Q = torch.empty(n, device=dev, dtype=torch.int64)
         self.feat = torch.empty(n, D, device=dev, dtype=torch.float32)
         self.sim = torch.empty(n, device=dev, dtype=torch.float32)
@@ -334,6 +357,17 @@ class ViTEngine:
                 if not last:
                     _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, s1, L["cqkv"], LNE, q2,
                          p1, eps)
+                elif self.cls_fused:
+                    # K, V never formed: the CLS query, G = W'_k^T q per head, the folded attention, then W'_v
+                    _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # the CLS rows' {mean, rstd}
+                    _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc,
+                         L["cqkv"][:D], LNE, qc)
+                    G, U = self.clsG[:n], self.clsU[:n]
+                    _run(T, "gemm_cls_g", vpf.gemm, qc, self.w_clsG, self.b_clsG, None, None, 0, None, None, BIAS, G)
+                    _run(T, "attention_cls", vpf.cls_attn_fold_, self.h[:n], pl, eps, G, qc, L["bqkv"][D:2 * D],
+                         A.heads, U)
+                    _run(T, "gemm_cls_v", vpf.gemm, U, self.w_clsV, L["bqkv"][2 * D:], None, None, 0, None, None,
+                         BIAS, xc)
                 elif self.fp8:
                     s8, p8 = ln_stats8(h2)
                     _run(T, "gemm_kv", vpf.gemm_mx8, h8q, h8s, *L["wkv8"], L["bqkv"][D:], None, s8, L["cqkv8"][D:],
@@ -356,7 +390,9 @@ class ViTEngine:
                          kv2)
                     _run(T, "gemm_q_cls", vpf.gemm, xc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, None, None,
                          BIAS, qc)
-            _run(T, "attention_cls" if last else "attention", vpf.attention, qkv, A.heads, 1 if last else N, self.x[:n])
+            if not (last and fold and self.cls_fused):
+                _run(T, "attention_cls" if last else "attention", vpf.attention, qkv, A.heads, 1 if last else N,
+                     self.x[:n])
             hh, xx, hd_, ss, pp = (hc, xc, hidc, stc, plc) if last else (h2, x2, hid, st, pl)
             tag = "_cls" if last else ""
             if fold:
