@@ -9,14 +9,18 @@
 // axpy per (token, head): this kernel. G comes from a block-diagonal GEMM of the CLS queries, and o from a
 // block-diagonal GEMM of U (vit.py).
 //
-// One 256-thread workgroup per particle; wave w takes tokens w, w+4, ...; lane l owns dims [H l, H l + H) of
-// every row (D = 64 H: a row is one coalesced 2D-byte wave load).
-//   pass 1: row statistics from the producer's statistics planes (kept in LDS), LNraw of the lane's dims, H
-//           partial dots with G (v_dot2_f32_bf16, G resident as bf16 pairs), a butterfly over the wave (all
-//           lanes end with the same bits) -> scores in LDS;
-//   softmax per head over the N scores (exact, two-pass, exp2 domain);
-//   pass 2: U_h += p_hj LNraw_j (H x H fp32 accumulators per lane), the four waves' partial U summed in LDS,
-//           out = U as bf16 [H][D] per particle.
+// One 256-thread workgroup (4 waves) per particle; the particle's N token rows stream through LDS once, in
+// chunks of 16 rows (double-buffered, register-staged: chunk c+2 is loaded while chunk c is consumed), and
+// both products run on MFMA against the raw bf16 rows, the LayerNorm applied algebraically per row:
+//   scores  S[t][h] = rstd_t (h_t . G_h - mean_t sum(G_h)) + c0_h       v_mfma_f32_16x16x32_bf16, rows = tokens,
+//           each wave a quarter of the D columns (its G slice resident: H/2 x 4 VGPRs), partials summed in LDS;
+//   softmax online over the chunks per head (running max with lazy rescale, as attention.hip), weights
+//           w_th = p_th rstd_t rounded to bf16, plus corr_h = sum_t w_th mean_t from the SAME rounded weights,
+//           so U_h = (sum_t w_th h_t - corr_h) / l_h = sum_t w_th (h_t - mean_t) / l_h exactly;
+//   U^T[dims][heads] += H_chunk^T W^T                                 v_mfma_f32_16x16x16_bf16, A operand by
+//           the hardware-transposed LDS read (ds_read_b64_tr_b16), each wave H 16-dim tiles of its quarter.
+// LDS chunk image: 16 rows of 2D bytes, 16-byte column chunk c of row r stored at c ^ (r & 15) (row reads of the
+// score operand conflict-free; the transposed reads 2-way). HBM traffic = the token rows once + planes + G.
 #include "vpf_common.h"
 #include "../../include/vpf.h"
 
@@ -24,8 +28,17 @@ using namespace vpf;
 
 namespace {
 
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int NMAX = 256;
+constexpr int CH = 16;   // token rows per chunk
+
+__device__ __forceinline__ bf16x4 lds_tr(const char* base, int off) {
+    typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+    const lds_v4* q = reinterpret_cast<const lds_v4*>((__attribute__((address_space(3))) const char*)((size_t)base) + off);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_v4*>(q));
+}
 
 template <int H>
 __global__ __launch_bounds__(256) void k_cls_attn_fold(const bf16_t* __restrict__ tok, int N,
@@ -35,139 +48,173 @@ __global__ __launch_bounds__(256) void k_cls_attn_fold(const bf16_t* __restrict_
                                                        const float* __restrict__ bk, float scale_log2,
                                                        bf16_t* __restrict__ out, int64_t ldo) {
     constexpr int D = 64 * H;
-    constexpr int HP = H / 2;   // bf16 pairs per lane slice of a row
-    __shared__ float sc[H][NMAX];          // scores, then probabilities
-    __shared__ float2 rs[NMAX];            // (mean, rstd) per token
-    __shared__ float usum[H * H * 64];     // the waves' partial U
-    __shared__ float c0s[H];
+    constexpr int ROWB = 2 * D;           // bytes per row
+    constexpr int RC = D / 8;             // 16-byte chunks per row
+    constexpr int QD = D / 4;             // columns per wave
+    constexpr int KS = QD / 32;           // score k-steps per wave (H / 2)
+    constexpr int UT = QD / 16;           // U tiles per wave (H)
+    constexpr int PIECES = CH * RC / 256; // staging chunks per thread (H / 2)
+    static_assert(RC % 16 == 0 && CH * RC % 256 == 0, "layout");
+    __shared__ __attribute__((aligned(16))) char img[2][CH * ROWB];
+    __shared__ float sp[4][CH][16];
+    __shared__ __attribute__((aligned(8))) bf16_t wl[16][CH];   // [head][token] bf16 weights (B operand)
+    __shared__ float alpha_s[16];
+    __shared__ float2 rs[NMAX];
+    __shared__ float c0s[16], gsum[16], lfin[16], cfin[16];
+
     const int p = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int g = lane >> 4, li = lane & 15;
     const bf16_t* trow0 = tok + (int64_t)p * N * D;
+    const bf16_t* Gp = G + (int64_t)p * ldg;
+    const int nc = (N + CH - 1) / CH;
 
-    // c0_h = q_h . b'_k,h (wave h % 4 reduces head h)
+    // staging registers: chunk rows -> LDS image
+    uint4 stg[PIECES];
+    auto load_chunk = [&](int c) {
+#pragma unroll
+        for (int k = 0; k < PIECES; ++k) {
+            const int piece = tid + 256 * k, r = piece / RC, col = piece % RC;
+            const int t = c * CH + r;
+            stg[k] = t < N ? *reinterpret_cast<const uint4*>(trow0 + (int64_t)t * D + col * 8) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store_chunk = [&](int b) {
+#pragma unroll
+        for (int k = 0; k < PIECES; ++k) {
+            const int piece = tid + 256 * k, r = piece / RC, col = piece % RC;
+            *reinterpret_cast<uint4*>(img[b] + r * ROWB + ((col ^ (r & 15)) << 4)) = stg[k];
+        }
+    };
+    load_chunk(0);
+
+    // prologue: row statistics from the planes, c0_h = q_h . bk_h, sum(G_h), this wave's G slice
+    if (tid < N) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int t = 0; t < H; ++t) {
+            const float2 st = *reinterpret_cast<const float2*>(planes + ((int64_t)t * plane_rows + (int64_t)p * N + tid) * 2);
+            s1 += st.x;
+            s2 += st.y;
+        }
+        const float mean = s1 * (1.0f / D);
+        rs[tid] = make_float2(mean, __builtin_amdgcn_rsqf(fmaxf(s2 * (1.0f / D) - mean * mean, 0.f) + eps));
+    }
     for (int h = wid; h < H; h += 4) {
         float a = bf2f(q[(int64_t)p * ldq + h * 64 + lane]) * bk[h * 64 + lane];
+        float gs = 0.f;
+        const uint32_t* gr = reinterpret_cast<const uint32_t*>(Gp + (int64_t)h * D) + lane * (H / 2);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-        if (lane == 0) c0s[h] = a;
+        for (int e = 0; e < H / 2; ++e) {
+            const uint32_t w = gr[e];
+            gs += bf2f((bf16_t)(w & 0xffff)) + bf2f((bf16_t)(w >> 16));
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            a += __shfl_xor(a, o, 64);
+            gs += __shfl_xor(gs, o, 64);
+        }
+        if (lane == 0) {
+            c0s[h] = a;
+            gsum[h] = gs;
+        }
     }
-    // G slice of this lane: H heads x H dims, bf16 pairs
-    uint32_t g[H][HP];
+    bf16x8 gf[KS];
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-        const uint32_t* gp = reinterpret_cast<const uint32_t*>(G + (int64_t)p * ldg + (int64_t)h * D + H * lane);
-#pragma unroll
-        for (int e = 0; e < HP; ++e) g[h][e] = gp[e];
+    for (int ks = 0; ks < KS; ++ks) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (li < H) v = *reinterpret_cast<const uint4*>(Gp + (int64_t)li * D + QD * wid + 32 * ks + 8 * g);
+        gf[ks] = __builtin_bit_cast(bf16x8, v);
     }
+    store_chunk(0);
+    if (nc > 1) load_chunk(1);
     __syncthreads();
 
-    // ---- pass 1: scores ----
-    for (int j = wid; j < N; j += 4) {
-        // row statistics: lane t < H (= the number of 64-column planes) fetches plane t, 16-lane butterfly
-        float2 st = make_float2(0.f, 0.f);
-        if (lane < H) st = *reinterpret_cast<const float2*>(planes + ((int64_t)lane * plane_rows + (int64_t)p * N + j) * 2);
-        float s1 = st.x, s2 = st.y;
+    f32x4 u[UT];
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            s1 += __shfl_xor(s1, o, 64);
-            s2 += __shfl_xor(s2, o, 64);
-        }
-        s1 = __shfl(s1, 0, 64);
-        s2 = __shfl(s2, 0, 64);
-        const float mean = s1 * (1.0f / D);
-        const float rstd = __builtin_amdgcn_rsqf(fmaxf(s2 * (1.0f / D) - mean * mean, 0.f) + eps);
-        if (lane == 0) rs[j] = make_float2(mean, rstd);
-        const uint32_t* rp = reinterpret_cast<const uint32_t*>(trow0 + (int64_t)j * D + H * lane);
-        uint32_t xb[HP];
-#pragma unroll
-        for (int e = 0; e < HP; ++e) {
-            const uint32_t w = rp[e];
-            xb[e] = pack_bf2((bf2f((bf16_t)(w & 0xffff)) - mean) * rstd, (bf2f((bf16_t)(w >> 16)) - mean) * rstd);
-        }
-        float s[H];
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-            float a = 0.f;
-#pragma unroll
-            for (int e = 0; e < HP; ++e)
-                a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, xb[e]),
-                                                   __builtin_bit_cast(bf16x2_t, g[h][e]), a, false);
-            s[h] = a;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-            for (int h = 0; h < H; ++h) s[h] += __shfl_xor(s[h], o, 64);
-        if (lane < H) {
-            float v = s[0];
-#pragma unroll
-            for (int h = 1; h < H; ++h) v = lane == h ? s[h] : v;
-            sc[lane][j] = v;
-        }
-    }
-    __syncthreads();
+    for (int t = 0; t < UT; ++t) u[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // softmax state of head ch = tid >> 4 (one 16-lane group per head; heads >= H stay empty)
+    const int ch = tid >> 4, ct = tid & 15;
+    float m = -INFINITY, l = 0.f, corr = 0.f;
 
-    // ---- softmax per head (exp2 domain, scale folded) ----
-    for (int h = wid; h < H; h += 4) {
-        const float c0 = c0s[h];
-        float mx = -INFINITY;
-        for (int j = lane; j < N; j += 64) mx = fmaxf(mx, (sc[h][j] + c0) * scale_log2);
+    for (int c = 0; c < nc; ++c) {
+        const char* buf = img[c & 1];
+        // ---- scores: S[token][head] partial over this wave's columns ----
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        float sum = 0.f;
-        for (int j = lane; j < N; j += 64) {
-            const float e = __builtin_amdgcn_exp2f((sc[h][j] + c0) * scale_log2 - mx);
-            sc[h][j] = e;
-            sum += e;
+        for (int ks = 0; ks < KS; ++ks) {
+            const int col = (QD / 8) * wid + 4 * ks + g;
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(buf + li * ROWB + ((col ^ li) << 4));
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, gf[ks], s, 0, 0, 0);
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-        const float inv = 1.0f / sum;
-        for (int j = lane; j < N; j += 64) sc[h][j] *= inv;
-    }
-    __syncthreads();
-
-    // ---- pass 2: U_h = sum_j p_hj LNraw_j ----
-    float u[H][H];
-#pragma unroll
-    for (int h = 0; h < H; ++h)
-#pragma unroll
-        for (int i = 0; i < H; ++i) u[h][i] = 0.f;
-    for (int j = wid; j < N; j += 4) {
-        const float2 mr = rs[j];
-        const uint32_t* rp = reinterpret_cast<const uint32_t*>(trow0 + (int64_t)j * D + H * lane);
-        float x[H];
-#pragma unroll
-        for (int e = 0; e < HP; ++e) {
-            const uint32_t w = rp[e];
-            x[2 * e] = (bf2f((bf16_t)(w & 0xffff)) - mr.x) * mr.y;
-            x[2 * e + 1] = (bf2f((bf16_t)(w >> 16)) - mr.x) * mr.y;
-        }
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-            const float pr = sc[h][j];
-#pragma unroll
-            for (int i = 0; i < H; ++i) u[h][i] = fmaf(pr, x[i], u[h][i]);
-        }
-    }
-    for (int w = 0; w < 4; ++w) {   // sum the waves' partial U (fixed order)
-        if (wid == w) {
-#pragma unroll
-            for (int h = 0; h < H; ++h)
-#pragma unroll
-                for (int i = 0; i < H; ++i) {
-                    float* up = &usum[(h * H + i) * 64 + lane];
-                    *up = w == 0 ? u[h][i] : *up + u[h][i];
-                }
-        }
+        for (int i = 0; i < 4; ++i) sp[wid][4 * g + i][li] = s[i];
         __syncthreads();
-    }
-    // out[h][H lane + i], as bf16 pairs; wave w writes heads w, w+4, ...
-    for (int h = wid; h < H; h += 4) {
-        uint32_t* op = reinterpret_cast<uint32_t*>(out + (int64_t)p * ldo + (int64_t)h * D + H * lane);
+        // ---- online softmax of this chunk (thread = (head ch, token ct)) ----
+        {
+            const int t = c * CH + ct;
+            float sc = -INFINITY;
+            float2 mr = make_float2(0.f, 0.f);
+            if (ch < H && t < N) {
+                mr = rs[t];
+                const float dot = sp[0][ct][ch] + sp[1][ct][ch] + sp[2][ct][ch] + sp[3][ct][ch];
+                sc = (mr.y * (dot - mr.x * gsum[ch]) + c0s[ch]) * scale_log2;
+            }
+            float cm = sc;
 #pragma unroll
-        for (int e = 0; e < HP; ++e)
-            op[e] = pack_bf2(usum[(h * H + 2 * e) * 64 + lane], usum[(h * H + 2 * e + 1) * 64 + lane]);
+            for (int o = 1; o < 16; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
+            // lazy rescale: the reference max only moves when the chunk max exceeds it by more than 8 (exp2 domain)
+            float alpha = 1.f;
+            if (cm > m + 8.f) {
+                alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m - cm);
+                m = cm;
+            }
+            const float pr = sc == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sc - m);
+            const bf16_t wb = f2bf(pr * mr.y);
+            float ps = pr, cs = bf2f(wb) * mr.x;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                ps += __shfl_xor(ps, o, 64);
+                cs += __shfl_xor(cs, o, 64);
+            }
+            l = l * alpha + ps;
+            corr = corr * alpha + cs;
+            wl[ch][ct] = wb;
+            if (ct == 0) alpha_s[ch] = alpha;
+        }
+        // ---- stage chunk c+1 (its buffer was last read before this iteration's first barrier) ----
+        if (c + 1 < nc) store_chunk((c + 1) & 1);
+        if (c + 2 < nc) load_chunk(c + 2);
+        __syncthreads();
+        // ---- U^T[dims][heads] = alpha U^T + H_chunk^T W^T ----
+        const float al = alpha_s[li];
+        if (__builtin_expect(__any(al != 1.f), 0)) {
+#pragma unroll
+            for (int t = 0; t < UT; ++t) u[t] *= al;
+        }
+        const bf16x4 wf = *reinterpret_cast<const bf16x4*>(&wl[li][4 * g]);
+        const int rq = 4 * g + (li >> 2), pp = li & 3;
+#pragma unroll
+        for (int t = 0; t < UT; ++t) {
+            const int c0 = (QD / 8) * wid + 2 * t + (pp >> 1);
+            const bf16x4 a = lds_tr(buf, rq * ROWB + ((c0 ^ rq) << 4) + (pp & 1) * 8);
+            u[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, wf, u[t], 0, 0, 0);
+        }
+    }
+    if (ct == 0 && ch < 16) {
+        lfin[ch] = l;
+        cfin[ch] = corr;
+    }
+    __syncthreads();
+    // out[head][dim] = (U - corr) / l: lane (head li, dims 4g .. 4g+3 of each tile)
+    if (li < H) {
+        const float inv = 1.0f / lfin[li], cr = cfin[li];
+        bf16_t* orow = out + (int64_t)p * ldo + (int64_t)li * D + QD * wid + 4 * g;
+#pragma unroll
+        for (int t = 0; t < UT; ++t)
+            *reinterpret_cast<uint2*>(orow + 16 * t) =
+                make_uint2(pack_bf2((u[t][0] - cr) * inv, (u[t][1] - cr) * inv),
+                           pack_bf2((u[t][2] - cr) * inv, (u[t][3] - cr) * inv));
     }
 }
 
@@ -180,8 +227,8 @@ VPF_API int vpf_cls_attn_fold_bf16(const uint16_t* tokens, int64_t n_part, int N
     if (n_part < 0 || N <= 0 || N > NMAX || !(H == 6 || H == 12) || !(eps >= 0.f)) return VPF_ERR_ARG;
     const int64_t D = 64 * H;
     if (!tokens || !planes || !G || !q || !bk || !out || plane_rows < n_part * N || ldg < H * D || ldq < D ||
-        ldo < H * D || (ldg & 1) || (ldo & 1) || n_part > INT32_MAX || ((uintptr_t)planes & 7) ||
-        ((uintptr_t)G & 3) || ((uintptr_t)out & 3) || ((uintptr_t)tokens & 3))
+        ldo < H * D || (ldg & 7) || (ldo & 3) || n_part > INT32_MAX || ((uintptr_t)planes & 7) ||
+        ((uintptr_t)G & 15) || ((uintptr_t)out & 7) || ((uintptr_t)tokens & 15))
         return VPF_ERR_ARG;
     if (n_part == 0) return 0;
     const float sl2 = scale * 1.44269504088896341f;

@@ -12,7 +12,9 @@
 //    XOR-swizzling the per-lane SOURCE address: 16-B chunk c of row r lives at physical chunk
 //    c ^ ((r >> 1) & 7) (tools/lds_banks.py: conflict-free for every 16-lane group).
 //  * One raw s_barrier per K-step behind a counted vmcnt (the next A K-tile stays in flight across it);
-//    right after it, the DMA for B(t+1) and A(t+2) is issued and flies while the 64 MFMAs per wave run.
+//    right after it the DMA for B(t+1) is issued; A(t+2)'s four DMA issues are interleaved into the 64 MFMAs
+//    per wave (one per 16), instead of running back to back after the barrier while the MFMA pipes idle
+//    (QKV / proj / FC1 / FC2 -0.2..-3 %, profiles/r1_gemm_lab/ilv_ab.txt).
 //  * MFMA operands are "swapped" (W fragment as A, activation fragment as B) so the accumulator holds
 //    D[n][m]: each lane owns 4 consecutive output columns of one row. Epilogue (gemm_common.h): bias
 //    (+ GELU, gelu_sig2) in fp32 on the accumulators, bf16 pack, 8-B writes into a per-wave XOR-swizzled
@@ -40,7 +42,7 @@ constexpr int AUX_PARTS = 15;
 constexpr int MAX_PARTS = 16;
 constexpr int AUX_BYTES = 2048 + AUX_PARTS * 2048;
 
-template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false>
+template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false, bool ILV = true>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W,
                                                         const float* __restrict__ bias,
@@ -178,12 +180,16 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             if (kt + 1 < nk) stage_b(kt + 1);
-            if (kt + 2 < nk) stage_a(kt + 2);
+            if (!ILV && kt + 2 < nk) stage_a(kt + 2);
             if (kt == (nk >= 2 ? nk - 2 : 0)) load_aux();
             if (wide && kt == nk - 1) load_planes(planes_lds);   // slot of A(nk-2): free after this barrier
             la = smem + (kt % 3) * OPERAND_BYTES;
             lb = smem + (3 + (kt & 1)) * OPERAND_BYTES;
         }
+        // ILV: A(t+2)'s DMA sits in the MFMA block, unconditionally (past the end it re-reads K-tile nk-1 into
+        // that K-tile's own slot: identical bytes), so its 4 issues interleave with the MFMAs instead of
+        // running back to back after the barrier. B(t+1) stays in its own block above, so it is always issued
+        // before A(t+2) and the counted vmcnt(4) keeps its meaning.
         // both 32-deep halves' fragments are read up front (24 ds_read_b128): the second half's reads
         // complete under the first half's 32 MFMAs instead of stalling between them
         bf16x8 a[2][8], b[2][4];
@@ -202,6 +208,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                 a[ks][i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + ch * 16);
             }
         }
+        // (after the reads in program order: a DMA into LDS may not be hoisted over them, MFMAs may pass it)
+        if constexpr (DEEP && ILV) stage_a(min(kt + 2, nk - 1));
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -209,8 +217,17 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
                     acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], a[ks][i], acc[j][i], 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads first
-        __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);   // then the 64 MFMAs (counted lgkmcnt waits)
+        if constexpr (DEEP && ILV) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads first
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {                          // then 16 MFMAs per A DMA issue
+                __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+        } else {
+            __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads first
+            __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);   // then the 64 MFMAs (counted lgkmcnt waits)
+        }
     }
 
     // ---------------- epilogue ----------------
@@ -269,6 +286,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     do {                                                                                                     \
         if (kern == 2)                                                                                       \
             hipLaunchKernelGGL((k_gemm_bf16<E, false>), grid, block, 0, s, VPF_GEMM_ARGS);                    \
+        else if (kern == 3 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
         else if (VPF_IS_LN(E) && stats_parts > AUX_PARTS)                                                    \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, VPF_IS_LN(E)>), grid, block, 0, s, VPF_GEMM_ARGS);       \
         else if (VPF_IS_PROD(E) && o8.q != nullptr)                                                          \
@@ -283,16 +302,17 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
     return g_group;
 }
 
-// GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring (product), 2 = the 2-stage ring (A/B timing).
+// GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, A's DMA interleaved into the MFMAs (product);
+// 2 = the 2-stage ring, 3 = the deep ring with both DMAs issued right after the barrier (A/B timing).
 // VPF_GEMM_KERNEL sets the initial value, vpf_gemm_tune() the current one.
 static int g_kernel = -1;
 static int gemm_kernel() {
-    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 2) g_kernel = 1; }
+    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 3) g_kernel = 1; }
     return g_kernel;
 }
 int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
 VPF_API int vpf_gemm_tune(int kernel, int group) {
-    if (kernel < 1 || kernel > 2) return VPF_ERR_ARG;
+    if (kernel < 1 || kernel > 3) return VPF_ERR_ARG;
     g_kernel = kernel;
     if (group >= 0) { tile_group(); g_group = group; }
     return 0;
