@@ -282,7 +282,9 @@ class ViTEngine:
         """L pre-norm blocks on h[:n]. The last block only needs the CLS rows after its attention (the
         final LN reads nothing else): its QKV GEMM computes K, V for every row but Q for the CLS rows only,
         its attention computes the CLS query only (q_rows = 1), and its proj / MLP run on the n strided CLS
-        rows."""
+        rows. With `cls_fused` (LN-folded bf16 / fp8, 6 or 12 heads) K and V are never formed: the CLS query
+        goes through W'_k per head (G), vpf_cls_attn_fold_bf16 reads the token rows once, and W'_v maps the
+        result back (csrc/cls_attn.hip)."""
         A = self.arch
         D, N, F = A.dim, A.tokens, A.mlp
         T = self.timer
