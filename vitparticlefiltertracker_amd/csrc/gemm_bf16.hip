@@ -12,9 +12,9 @@
 //    XOR-swizzling the per-lane SOURCE address: 16-B chunk c of row r lives at physical chunk
 //    c ^ ((r >> 1) & 7) (tools/lds_banks.py: conflict-free for every 16-lane group).
 //  * One raw s_barrier per K-step behind a counted vmcnt (the next A K-tile stays in flight across it);
-//    right after it the DMA for B(t+1) is issued; A(t+2)'s four DMA issues are interleaved into the 64 MFMAs
-//    per wave (one per 16), instead of running back to back after the barrier while the MFMA pipes idle
-//    (QKV / proj / FC1 / FC2 -0.2..-3 %, profiles/r1_gemm_lab/ilv_ab.txt).
+//    the refills are issued from the MFMA block: B(t+1)'s DMA right behind the fragment reads, A(t+2)'s four
+//    issues interleaved into the 64 MFMAs per wave (one per 16), instead of 8 back-to-back issues after the
+//    barrier while the MFMA pipes idle (QKV / proj / FC1 / FC2 -1.8..-4.5 %, profiles/r1_gemm_lab/ilv_ab.txt).
 //  * MFMA operands are "swapped" (W fragment as A, activation fragment as B) so the accumulator holds
 //    D[n][m]: each lane owns 4 consecutive output columns of one row. Epilogue (gemm_common.h): bias
 //    (+ GELU, gelu_sig2) in fp32 on the accumulators, bf16 pack, 8-B writes into a per-wave XOR-swizzled
@@ -179,17 +179,13 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            if (kt + 1 < nk) stage_b(kt + 1);
+            if (!ILV && kt + 1 < nk) stage_b(kt + 1);
             if (!ILV && kt + 2 < nk) stage_a(kt + 2);
             if (kt == (nk >= 2 ? nk - 2 : 0)) load_aux();
             if (wide && kt == nk - 1) load_planes(planes_lds);   // slot of A(nk-2): free after this barrier
             la = smem + (kt % 3) * OPERAND_BYTES;
             lb = smem + (3 + (kt & 1)) * OPERAND_BYTES;
         }
-        // ILV: A(t+2)'s DMA sits in the MFMA block, unconditionally (past the end it re-reads K-tile nk-1 into
-        // that K-tile's own slot: identical bytes), so its 4 issues interleave with the MFMAs instead of
-        // running back to back after the barrier. B(t+1) stays in its own block above, so it is always issued
-        // before A(t+2) and the counted vmcnt(4) keeps its meaning.
         // both 32-deep halves' fragments are read up front (24 ds_read_b128): the second half's reads
         // complete under the first half's 32 MFMAs instead of stalling between them
         bf16x8 a[2][8], b[2][4];
@@ -208,8 +204,16 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                 a[ks][i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + ch * 16);
             }
         }
-        // (after the reads in program order: a DMA into LDS may not be hoisted over them, MFMAs may pass it)
-        if constexpr (DEEP && ILV) stage_a(min(kt + 2, nk - 1));
+        // ILV: the refills are issued from the MFMA block, after the fragment reads in program order (a DMA into
+        // LDS is never hoisted over an LDS read; MFMAs may pass it): B(t+1)'s 4 issues right behind the reads,
+        // whose latency they overlap, then A(t+2)'s 4 interleaved one per 16 MFMAs, instead of 8 back-to-back
+        // issues after the barrier while the MFMA pipes idle. Unconditional, so they stay in this block: past
+        // the end they re-read K-tile nk-1 into that K-tile's own slot (identical bytes). Program order B, A
+        // keeps the counted vmcnt(4) at the next barrier meaning "B(t+1) has landed".
+        if constexpr (DEEP && ILV) {
+            stage_b(min(kt + 1, nk - 1));
+            stage_a(min(kt + 2, nk - 1));
+        }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -218,9 +222,10 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                 for (int i = 0; i < 8; ++i)
                     acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], a[ks][i], acc[j][i], 0, 0, 0);
         if constexpr (DEEP && ILV) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads first
+            __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads
+            __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);    // B(t+1)'s DMA
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {                          // then 16 MFMAs per A DMA issue
+            for (int q = 0; q < 4; ++q) {                          // 16 MFMAs per A(t+2) DMA issue
                 __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
                 __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
             }
@@ -302,8 +307,8 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
     return g_group;
 }
 
-// GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, A's DMA interleaved into the MFMAs (product);
-// 2 = the 2-stage ring, 3 = the deep ring with both DMAs issued right after the barrier (A/B timing).
+// GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, refills issued from the MFMA block (product);
+// 2 = the 2-stage ring, 3 = the deep ring with both refills issued right after the barrier (A/B timing).
 // VPF_GEMM_KERNEL sets the initial value, vpf_gemm_tune() the current one.
 static int g_kernel = -1;
 static int gemm_kernel() {
