@@ -343,7 +343,8 @@ def test_attention_q_rows(dtype, B, N, H):
     assert torch.all(part2[:, 2:] == 5.0)
 
 
-@pytest.mark.parametrize("B,N,H", [(3, 197, 12), (5, 197, 6), (2, 256, 12), (4, 1, 6), (64, 50, 12)])
+@pytest.mark.parametrize("B,N,H", [(3, 197, 12), (5, 197, 6), (2, 256, 12), (4, 1, 6), (64, 50, 12), (2, 577, 16),
+                                   (3, 640, 16)])
 def test_cls_attn_fold(B, N, H):
     """The last block's CLS attention with K / V never formed (vpf_cls_attn_fold_bf16) against an fp64
     restatement: LNraw from the statistics planes, s_hj = (LNraw_j . G_h + q_h . bk_h) / 8, U_h = sum_j p_hj
@@ -392,15 +393,15 @@ def test_cls_attn_fold_argument_contract():
     from vitparticlefiltertracker_amd._lib import VPFError
     with pytest.raises((ValueError, VPFError)):
         vpf().cls_attn_fold_(h, planes[:, :B * N - 1], 1e-6, G, q, bk, H, out)       # planes too short
-    h16 = torch.zeros(B, N, 1024, device=DEV, dtype=torch.bfloat16)
+    h8 = torch.zeros(B, N, 512, device=DEV, dtype=torch.bfloat16)
     with pytest.raises((ValueError, VPFError)):
-        vpf().cls_attn_fold_(h16, torch.zeros(16, B * N, 2, device=DEV), 1e-6, torch.zeros(B, 16 * 1024, device=DEV,
-                             dtype=torch.bfloat16), torch.zeros(B, 1024, device=DEV, dtype=torch.bfloat16),
-                             torch.zeros(1024, device=DEV), 16, torch.empty(B, 16 * 1024, device=DEV,
-                                                                            dtype=torch.bfloat16))   # H = 16
-    h300 = torch.zeros(1, 300, D, device=DEV, dtype=torch.bfloat16)
+        vpf().cls_attn_fold_(h8, torch.zeros(8, B * N, 2, device=DEV), 1e-6, torch.zeros(B, 8 * 512, device=DEV,
+                             dtype=torch.bfloat16), torch.zeros(B, 512, device=DEV, dtype=torch.bfloat16),
+                             torch.zeros(512, device=DEV), 8, torch.empty(B, 8 * 512, device=DEV,
+                                                                          dtype=torch.bfloat16))   # H = 8
+    h700 = torch.zeros(1, 700, D, device=DEV, dtype=torch.bfloat16)
     with pytest.raises((ValueError, VPFError)):
-        vpf().cls_attn_fold_(h300, torch.zeros(H, 300, 2, device=DEV), 1e-6, G[:1], q[:1], bk, H, out[:1])  # N > 256
+        vpf().cls_attn_fold_(h700, torch.zeros(H, 700, 2, device=DEV), 1e-6, G[:1], q[:1], bk, H, out[:1])  # N > 640
 
 
 @pytest.mark.parametrize("mode", ["0", "2"])

@@ -51,7 +51,8 @@ def test_vit_features_vs_oracle(name, dtype, n):
         assert cos.min().item() > (0.999 if dtype == "bf16" else 0.99), cos
 
 
-@pytest.mark.parametrize("name,dtype", [("vit_base_patch16_224", "bf16"), ("vit_small_patch16_224", "fp8")])
+@pytest.mark.parametrize("name,dtype", [("vit_base_patch16_224", "bf16"), ("vit_small_patch16_224", "fp8"),
+                                        ("vit_large_patch14_336", "bf16")])
 def test_cls_fused_tail_equals_kv_path(name, dtype, monkeypatch):
     """The last block's CLS attention without K / V (vpf_cls_attn_fold_bf16 between two block-diagonal GEMMs)
     against the K / V GEMM + attention path it replaces (VPF_CLS_FUSED=0), and both against the fp32 oracle."""

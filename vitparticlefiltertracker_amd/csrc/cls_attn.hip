@@ -31,7 +31,7 @@ namespace {
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int NMAX = 256;
+constexpr int NMAX = 640;   // tokens (ViT-L/14 @ 336: 577)
 constexpr int CH = 16;   // token rows per chunk
 
 __device__ __forceinline__ bf16x4 lds_tr(const char* base, int off) {
@@ -89,16 +89,16 @@ __global__ __launch_bounds__(256) void k_cls_attn_fold(const bf16_t* __restrict_
     load_chunk(0);
 
     // prologue: row statistics from the planes, c0_h = q_h . bk_h, sum(G_h), this wave's G slice
-    if (tid < N) {
+    for (int j = tid; j < N; j += 256) {
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int t = 0; t < H; ++t) {
-            const float2 st = *reinterpret_cast<const float2*>(planes + ((int64_t)t * plane_rows + (int64_t)p * N + tid) * 2);
+            const float2 st = *reinterpret_cast<const float2*>(planes + ((int64_t)t * plane_rows + (int64_t)p * N + j) * 2);
             s1 += st.x;
             s2 += st.y;
         }
         const float mean = s1 * (1.0f / D);
-        rs[tid] = make_float2(mean, __builtin_amdgcn_rsqf(fmaxf(s2 * (1.0f / D) - mean * mean, 0.f) + eps));
+        rs[j] = make_float2(mean, __builtin_amdgcn_rsqf(fmaxf(s2 * (1.0f / D) - mean * mean, 0.f) + eps));
     }
     for (int h = wid; h < H; h += 4) {
         float a = bf2f(q[(int64_t)p * ldq + h * 64 + lane]) * bk[h * 64 + lane];
@@ -224,7 +224,7 @@ VPF_API int vpf_cls_attn_fold_bf16(const uint16_t* tokens, int64_t n_part, int N
                                    int64_t plane_rows, float eps, const uint16_t* G, int64_t ldg, const uint16_t* q,
                                    int64_t ldq, const float* bk, float scale, uint16_t* out, int64_t ldo,
                                    void* stream) {
-    if (n_part < 0 || N <= 0 || N > NMAX || !(H == 6 || H == 12) || !(eps >= 0.f)) return VPF_ERR_ARG;
+    if (n_part < 0 || N <= 0 || N > NMAX || !(H == 6 || H == 12 || H == 16) || !(eps >= 0.f)) return VPF_ERR_ARG;
     const int64_t D = 64 * H;
     if (!tokens || !planes || !G || !q || !bk || !out || plane_rows < n_part * N || ldg < H * D || ldq < D ||
         ldo < H * D || (ldg & 7) || (ldo & 3) || n_part > INT32_MAX || ((uintptr_t)planes & 7) ||
@@ -237,7 +237,10 @@ VPF_API int vpf_cls_attn_fold_bf16(const uint16_t* tokens, int64_t n_part, int N
     const bf16_t* g = reinterpret_cast<const bf16_t*>(G);
     const bf16_t* qq = reinterpret_cast<const bf16_t*>(q);
     bf16_t* o = reinterpret_cast<bf16_t*>(out);
-    if (H == 12)
+    if (H == 16)
+        hipLaunchKernelGGL(k_cls_attn_fold<16>, dim3((unsigned)n_part), dim3(256), 0, s, t, N, planes, plane_rows,
+                           eps, g, ldg, qq, ldq, bk, sl2, o, ldo);
+    else if (H == 12)
         hipLaunchKernelGGL(k_cls_attn_fold<12>, dim3((unsigned)n_part), dim3(256), 0, s, t, N, planes, plane_rows,
                            eps, g, ldg, qq, ldq, bk, sl2, o, ldo);
     else

@@ -163,12 +163,12 @@ class ViTEngine:
         self.ng = f32(weights["norm.weight"])
         self.nb = f32(weights["norm.bias"])
         # the last block's CLS attention without K / V (vpf_cls_attn_fold_bf16): LN-folded bf16 with statistics
-        # planes, head dim 64, 6 or 12 heads, N <= 256. Two block-diagonal weights carry the per-head algebra:
+        # planes, head dim 64, 6, 12 or 16 heads, N <= 640. Two block-diagonal weights carry the per-head algebra:
         #   G[p][h D + i] = sum_{k in head h} q[p][k] W'_k[k][i]        (W_G[h D + i][k] = W'_k[k][i])
         #   x[p][64 h + d] = sum_i W'_v[64 h + d][i] U[p][h D + i] + b'_v (W_V[64 h + d][h D + i] = W'_v[64 h + d][i])
         # VPF_CLS_FUSED=0 keeps the K / V GEMM + attention path (A/B, tests).
         H = A.heads
-        self.cls_fused = (self.fold_ln and H in (6, 12) and D == 64 * H and N <= 256
+        self.cls_fused = (self.fold_ln and H in (6, 12, 16) and D == 64 * H and N <= 640
                           and os.environ.get("VPF_CLS_FUSED", "1") != "0")
         if self.cls_fused:
             L = self.layers[-1]
@@ -282,7 +282,7 @@ class ViTEngine:
         """L pre-norm blocks on h[:n]. The last block only needs the CLS rows after its attention (the
         final LN reads nothing else): its QKV GEMM computes K, V for every row but Q for the CLS rows only,
         its attention computes the CLS query only (q_rows = 1), and its proj / MLP run on the n strided CLS
-        rows. With `cls_fused` (LN-folded bf16 / fp8, 6 or 12 heads) K and V are never formed: the CLS query
+        rows. With `cls_fused` (LN-folded bf16 / fp8, 6, 12 or 16 heads) K and V are never formed: the CLS query
         goes through W'_k per head (G), vpf_cls_attn_fold_bf16 reads the token rows once, and W'_v maps the
         result back (csrc/cls_attn.hip)."""
         A = self.arch
