@@ -66,8 +66,8 @@ def main():
         times = {k: [] for k in kerns}
         out = res0.clone()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        for _ in range(rounds):
-            for k in kerns:
+        for r in range(rounds):
+            for k in (kerns if r % 2 == 0 else kerns[::-1]):   # alternate the order: no position bias
                 L.vpf_gemm_tune(k, GROUP)
                 ev[0].record()
                 for _ in range(3):

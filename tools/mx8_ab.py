@@ -57,13 +57,22 @@ def main():
             f16 = lambda: V.gemm_stats_(a, w, bias, out, None, 0, E.VPF_EPI_BIAS_RESIDUAL, out, pl_out)  # noqa
             f8 = lambda: V.gemm_q8_(a, w, bias, out, None, 0, E.VPF_EPI_BIAS_RESIDUAL, out, pl_out, q8, s8)  # noqa
         fns = {"bf16": f16, "mx8" if name != "proj" else "bf16+q8": f8}
+        for v in [x for x in os.environ.get("AB_MX8_VARIANTS", "").split(",") if x]:
+            def fv(v=v, f8=f8):   # same call under VPF_MX8_VARIANT=v (read by the library at each launch)
+                os.environ["VPF_MX8_VARIANT"] = v
+                f8()
+                os.environ.pop("VPF_MX8_VARIANT")
+            fns["mx8_v" + v] = fv
+        if os.environ.get("AB_NO_BF16"):   # variant A/B only: the bf16 call's own operands would cool the MALL
+            fns.pop("bf16")
         for f in fns.values():
             f()
         torch.cuda.synchronize()
         times = {k: [] for k in fns}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        for _ in range(rounds):
-            for k, f in fns.items():
+        for r in range(rounds):
+            order = list(fns.items())
+            for k, f in (order if r % 2 == 0 else order[::-1]):   # alternate the order: no position bias
                 ev[0].record()
                 for _ in range(3):
                     f()

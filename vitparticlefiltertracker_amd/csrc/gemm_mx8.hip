@@ -46,7 +46,7 @@ __device__ __forceinline__ void mx_col(f32x4 (&acc)[8], const i32x8& b, const i3
 }
 #undef VPF_MX
 
-template <int EPI, bool OUT8>
+template <int EPI, bool OUT8, bool EARLY = true>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict__ A, int lda,
                                                        const uint32_t* __restrict__ As, int lds_a,
                                                        const uint8_t* __restrict__ W,
@@ -178,8 +178,6 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
                      : "+v"(al[0]), "+v"(al[1]), "+v"(al[2]), "+v"(al[3]), "+v"(al[4]), "+v"(al[5]), "+v"(al[6]),
                        "+v"(al[7]), "+v"(ah[0]), "+v"(ah[1]), "+v"(ah[2]), "+v"(ah[3]), "+v"(ah[4]), "+v"(ah[5]),
                        "+v"(ah[6]), "+v"(ah[7]));
-        __builtin_amdgcn_s_barrier();   // every wave holds K-tile kt in registers: its buffer is free
-        asm volatile("" ::: "memory");
         i32x8 a[8], b[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -187,6 +185,26 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             a[i] = i32x8{al[i].x, al[i].y, al[i].z, al[i].w, ah[i].x, ah[i].y, ah[i].z, ah[i].w};
+        if constexpr (EARLY) {
+            // the first column group's 8 MFMAs run before the buffer-release barrier (they need only registers),
+            // so the MFMA pipe works while the slower waves finish their reads
+            mx_col<0>(acc[0], b[0], a, sb, sa0, sa1);
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            stage(kt & 1, min(kt + 2, nk - 1));
+            mx_col<1>(acc[1], b[1], a, sb, sa0, sa1);
+            mx_col<2>(acc[2], b[2], a, sb, sa0, sa1);
+            mx_col<3>(acc[3], b[3], a, sb, sa0, sa1);
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {   // one DMA issue after every 2 MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            continue;
+        }
+        __builtin_amdgcn_s_barrier();   // every wave holds K-tile kt in registers: its buffer is free
+        asm volatile("" ::: "memory");
         stage(kt & 1, min(kt + 2, nk - 1));
         // swapped operands as in the bf16 kernel: W fragment as MFMA-A, activation as MFMA-B -> D[n][m]
         mx_col<0>(acc[0], b[0], a, sb, sa0, sa1);
@@ -260,8 +278,12 @@ __global__ __launch_bounds__(256) void k_quantize_mx8(const bf16_t* __restrict__
         C, (int)ldc, (int)M, (int)N, (int)K, group, stats_parts, ln_eps, stats_out, o8
 #define VPF_MX8_LAUNCH(E)                                                                                    \
     do {                                                                                                     \
-        if (o8.q)                                                                                            \
+        if (o8.q && late)                                                                                    \
+            hipLaunchKernelGGL((k_gemm_mx8<E, true, false>), grid, block, 0, s, VPF_MX8_ARGS);                \
+        else if (o8.q)                                                                                       \
             hipLaunchKernelGGL((k_gemm_mx8<E, true>), grid, block, 0, s, VPF_MX8_ARGS);                       \
+        else if (late)                                                                                       \
+            hipLaunchKernelGGL((k_gemm_mx8<E, false, false>), grid, block, 0, s, VPF_MX8_ARGS);               \
         else                                                                                                 \
             hipLaunchKernelGGL((k_gemm_mx8<E, false>), grid, block, 0, s, VPF_MX8_ARGS);                      \
     } while (0)
@@ -291,6 +313,9 @@ VPF_API int vpf_gemm_mx8(const uint8_t* A, int64_t lda, const uint32_t* As, int6
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)tiles), block(NTHREADS);
     const int group = vpf_gemm_tile_group();
+    // VPF_MX8_VARIANT=0: the previous schedule (all MFMAs after the buffer-release barrier), for A/B timing
+    const char* var = getenv("VPF_MX8_VARIANT");
+    const bool late = var && var[0] == '0';
     switch (epilogue) {
         case VPF_EPI_BIAS: VPF_MX8_LAUNCH(VPF_EPI_BIAS); break;
         case VPF_EPI_BIAS_GELU: VPF_MX8_LAUNCH(VPF_EPI_BIAS_GELU); break;
