@@ -3,7 +3,7 @@
 kernel 2 (k_gemm_bf16_t2, two 256x128-tile workgroups per CU), interleaved rounds in one process
 (cdna_hip_programming.md §5.4 rule 24), random operands, outputs compared bit for bit.
 
-usage: python tools/gemm_ab.py [rounds] [shapes comma list] [kernels comma list]
+usage: python tools/gemm_ab.py [rounds] [shapes comma list] [variants comma list: k or k:group]
 """
 import os
 import sys
@@ -30,7 +30,12 @@ SHAPES = {  # name: (N, K, epilogue)
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     names = sys.argv[2].split(",") if len(sys.argv) > 2 and sys.argv[2] else list(SHAPES)
-    kerns = [int(k) for k in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 2]
+    # variants "k" or "k:g" (kernel k with tile-order group g)
+    kerns = sys.argv[3].split(",") if len(sys.argv) > 3 else ["1", "2"]
+
+    def tune(v):
+        k, _, g = v.partition(":")
+        return L.vpf_gemm_tune(int(k), int(g) if g else GROUP)
     M = int(os.environ.get("AB_M", 4096 * 197))
     dev = "cuda:0"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -54,7 +59,7 @@ def main():
                      epi, out)
 
         for k in kerns:
-            assert L.vpf_gemm_tune(k, GROUP) == 0
+            assert tune(k) == 0
             out = res0.clone()
             run(out)
             torch.cuda.synchronize()
@@ -68,7 +73,7 @@ def main():
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for r in range(rounds):
             for k in (kerns if r % 2 == 0 else kerns[::-1]):   # alternate the order: no position bias
-                L.vpf_gemm_tune(k, GROUP)
+                tune(k)
                 ev[0].record()
                 for _ in range(3):
                     run(out)
