@@ -42,7 +42,7 @@ constexpr int AUX_PARTS = 15;
 constexpr int MAX_PARTS = 16;
 constexpr int AUX_BYTES = 2048 + AUX_PARTS * 2048;
 
-template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false, bool ILV = true>
+template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false, bool ILV = true, bool PIPED_EPI = true>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W,
                                                         const float* __restrict__ bias,
@@ -273,9 +273,14 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         const int region = (wid >> 1) + ((wid >> 1) >= (nk % 3) ? 1 : 0);
         img = smem + region * OPERAND_BYTES + (wid & 1) * 16384;
     }
-    float* prod_stats = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) ? stats_out : nullptr;
-    store_wave_tile<EPI, OUT8>(img, aux, acc, wm, wn, m0, n0, lane, res, pos, g2, C, ldc, M, N, prod_stats,
-                               stats_rows, o8);
+    if constexpr (PIPED_EPI && EPI != VPF_EPI_PATCH && !OUT8) {
+        store_wave_tile_pipe<EPI>(img, aux, acc, wm, wn, m0, n0, lane, res, C, ldc, M, N,
+                                  EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr, stats_rows);
+    } else {
+        float* prod_stats = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) ? stats_out : nullptr;
+        store_wave_tile<EPI, OUT8>(img, aux, acc, wm, wn, m0, n0, lane, res, pos, g2, C, ldc, M, N, prod_stats,
+                                   stats_rows, o8);
+    }
 }
 
 }  // namespace
@@ -293,6 +298,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             hipLaunchKernelGGL((k_gemm_bf16<E, false>), grid, block, 0, s, VPF_GEMM_ARGS);                    \
         else if (kern == 3 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
+        else if (kern == 4 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
         else if (VPF_IS_LN(E) && stats_parts > AUX_PARTS)                                                    \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, VPF_IS_LN(E)>), grid, block, 0, s, VPF_GEMM_ARGS);       \
         else if (VPF_IS_PROD(E) && o8.q != nullptr)                                                          \
@@ -312,12 +319,12 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
 // VPF_GEMM_KERNEL sets the initial value, vpf_gemm_tune() the current one.
 static int g_kernel = -1;
 static int gemm_kernel() {
-    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 3) g_kernel = 1; }
+    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 4) g_kernel = 1; }
     return g_kernel;
 }
 int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
 VPF_API int vpf_gemm_tune(int kernel, int group) {
-    if (kernel < 1 || kernel > 3) return VPF_ERR_ARG;
+    if (kernel < 1 || kernel > 4) return VPF_ERR_ARG;
     g_kernel = kernel;
     if (group >= 0) { tile_group(); g_group = group; }
     return 0;

@@ -145,6 +145,111 @@ __device__ __forceinline__ void epi_to_image(char* img, const char* aux, const f
     }
 }
 
+// Pipelined form of epi_to_image + store_wave_tile for the epilogues with a bf16 output only (EPI_BIAS / BIAS_GELU /
+// LN / LN_GELU / BIAS_RESIDUAL with its statistics planes): fragment row-group i's math and image rows, then that group's two 16-B store iterations, so
+// the stores start after the first 16 rows instead of after all 128 and drain under the remaining math. Same image
+// layout and store pattern as the two-pass form (bit-identical output).
+template <int EPI>
+__device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm,
+                                                     int wn, int m0, int n0, int lane, const uint4 (&res)[16],
+                                                     bf16_t* C, int ldc, int M, int N, float* stats_out,
+                                                     int stats_rows) {
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    constexpr bool RES = EPI == VPF_EPI_BIAS_RESIDUAL;
+    const int fr = lane & 15, fq = lane >> 4, c16 = lane & 7;
+    float4 bv[4], cv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = (wn * 64 + j * 16 + fq * 4) * 4;
+        bv[j] = *reinterpret_cast<const float4*>(aux + c);
+        if constexpr (LN) cv[j] = *reinterpret_cast<const float4*>(aux + 1024 + c);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        f32x2 rsx = {1.f, 1.f}, rsy = {0.f, 0.f};
+        if constexpr (LN) {
+            const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + (wm * 128 + i * 16 + fr) * 8);
+            rsx = f32x2{st.y, st.y};
+            rsy = f32x2{-st.y * st.x, -st.y * st.x};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f32x2 v01, v23;
+            const f32x2 a01 = {acc[j][i][0], acc[j][i][1]}, a23 = {acc[j][i][2], acc[j][i][3]};
+            const f32x2 b01 = {bv[j].x, bv[j].y}, b23 = {bv[j].z, bv[j].w};
+            if constexpr (LN) {
+                const f32x2 c01 = {cv[j].x, cv[j].y}, c23 = {cv[j].z, cv[j].w};
+                v01 = __builtin_elementwise_fma(rsx, a01, __builtin_elementwise_fma(rsy, c01, b01));
+                v23 = __builtin_elementwise_fma(rsx, a23, __builtin_elementwise_fma(rsy, c23, b23));
+            } else {
+                v01 = a01 + b01;
+                v23 = a23 + b23;
+            }
+            if constexpr (EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU) {
+                v01 = gelu_sig2(v01);
+                v23 = gelu_sig2(v23);
+            }
+            const int row = i * 16 + fr;
+            const int c8 = (j * 4 + fq) ^ (row & 15);
+            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
+                make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
+        }
+        __builtin_amdgcn_wave_barrier();   // the image is private to this wave: LDS ops of one wave stay in order
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = (2 * i + h) * 8 + (lane >> 3);   // rows of group i only
+            uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+            if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+            const int m = m0 + wm * 128 + row;
+            const int n = n0 + wn * 64 + c16 * 8;
+            const bool ok = m < M && n < N;
+            if constexpr (RES) {
+                const uint4 rv = res[2 * i + h];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+                uint32_t o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    o[e] = pack_bf2(bf2f((bf16_t)(w[e] & 0xffff)) + bf2f((bf16_t)(rr[e] & 0xffff)),
+                                    bf2f((bf16_t)(w[e] >> 16)) + bf2f((bf16_t)(rr[e] >> 16)));
+                v = make_uint4(o[0], o[1], o[2], o[3]);
+                if (stats_out != nullptr) {   // wave-uniform; as store_wave_tile: the lane's partial back into its row
+                    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+                    const bf16x2_t one2 = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
+                    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, o[e]);
+                        s1 = __builtin_amdgcn_fdot2_f32_bf16(pr, one2, s1, false);
+                        s2 = __builtin_amdgcn_fdot2_f32_bf16(pr, pr, s2, false);
+                    }
+                    if (!ok) { s1 = 0.f; s2 = 0.f; }
+                    *reinterpret_cast<float2*>(img + row * 128 + c16 * 8) = make_float2(s1, s2);
+                }
+            }
+            if (ok) *reinterpret_cast<uint4*>(C + (int64_t)m * ldc + n) = v;
+        }
+    }
+    if constexpr (RES) {
+        const int nb = n0 + wn * 64;
+        if (stats_out != nullptr && nb < N) {   // wave-uniform: rows 2 lane, 2 lane + 1, 8 partials each
+            __builtin_amdgcn_wave_barrier();
+            float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 u0 = *reinterpret_cast<const float4*>(img + (2 * lane) * 128 + q * 16);
+                const float4 u1 = *reinterpret_cast<const float4*>(img + (2 * lane + 1) * 128 + q * 16);
+                t.x += u0.x + u0.z; t.y += u0.y + u0.w;
+                t.z += u1.x + u1.z; t.w += u1.y + u1.w;
+            }
+            float* plane = stats_out + (int64_t)(nb >> 6) * stats_rows * 2;
+            const int m = m0 + wm * 128 + 2 * lane;
+            if (m + 1 < M) *reinterpret_cast<float4*>(plane + (int64_t)m * 2) = t;
+            else if (m < M) *reinterpret_cast<float2*>(plane + (int64_t)m * 2) = make_float2(t.x, t.y);
+        }
+    }
+}
+
 // The residual rows a lane adds in store_wave_tile (EPI_BIAS_RESIDUAL): 16 x 16 B, all in flight at once. The
 // kernels issue this right after their K loop, before the epilogue barrier (a raw s_barrier, so the loads stay
 // in flight across it), which gives them the LN combine, the barrier and the image writes to land under.
