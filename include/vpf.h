@@ -147,10 +147,14 @@ int vpf_attention_f32(const float* qkv, float* out, int64_t B, int N, int H, int
 /* H6 for the last block's CLS query with K and V never materialised (LN-folded bf16 mode). With
  * LNraw_j = (h_j - mean_j) rstd_j (statistics from the planes, as vpf_gemm_bf16's stats_parts), G_h the D-vector
  * W'_k,h^T q_h and c0_h = q_h . bk_h:  p_h = softmax_j((LNraw_j . G_h + c0_h) scale),  out_h = sum_j p_hj LNraw_j.
- * The caller finishes o_h = W'_v,h out_h + b'_v,h with one GEMM (vit.py).
+ * The caller finishes o_h = W'_v,h out_h + b'_v,h with one GEMM over the [n*H][D] rows of out and
+ * vpf_head_gather_bf16 (vit.py).
  * tokens: bf16 [n_part][N][D] contiguous (D = 64 H, H in {6, 12, 16}, N <= 640); planes: fp32 [H][plane_rows][2]
  * {sum, sumsq} per 64-column block, row p*N + j; G: bf16 rows of ldg >= H*D ([h][D] per particle);
  * q: bf16 CLS queries (row stride ldq); bk: fp32[D]; out: bf16 rows of ldo >= H*D ([h][D]). */
+/* out[p][h*hd + d] = Y[p*H + h][h*hd + d] for p < n (the diagonal blocks of a per-(particle, head) projection
+ * Y: bf16 [n*H][H*hd] contiguous); out rows of ldo >= H*hd elements. hd % 8 == 0, 16-B aligned pointers. */
+int vpf_head_gather_bf16(const uint16_t* Y, int64_t n, int H, int hd, uint16_t* out, int64_t ldo, void* stream);
 int vpf_cls_attn_fold_bf16(const uint16_t* tokens, int64_t n_part, int N, int H, const float* planes,
                            int64_t plane_rows, float eps, const uint16_t* G, int64_t ldg, const uint16_t* q,
                            int64_t ldq, const float* bk, float scale, uint16_t* out, int64_t ldo, void* stream);

@@ -382,6 +382,19 @@ def test_cls_attn_fold(B, N, H):
     torch.testing.assert_close(o, o_ref, rtol=3e-2, atol=2e-2 * o_ref.abs().max().item())
 
 
+@pytest.mark.parametrize("n,H", [(5, 12), (1, 6), (33, 16)])
+def test_head_gather(n, H):
+    """vpf_head_gather_bf16: out[p][h hd + d] = Y[p H + h][h hd + d], into row-strided output; bit-exact."""
+    D = 64 * H
+    Y = torch.randn(n * H, D, device=DEV).to(torch.bfloat16)
+    big = torch.full((n, 3 * D), 9.0, device=DEV, dtype=torch.bfloat16)
+    out = big[:, D:2 * D]
+    vpf().head_gather_(Y, H, out)
+    ref = torch.stack([Y.view(n, H, D)[:, h, 64 * h:64 * h + 64] for h in range(H)], 1).reshape(n, D)
+    assert torch.equal(out, ref)
+    assert torch.all(big[:, :D] == 9.0) and torch.all(big[:, 2 * D:] == 9.0)
+
+
 def test_cls_attn_fold_argument_contract():
     H, D, B, N = 12, 768, 2, 197
     h = torch.zeros(B, N, D, device=DEV, dtype=torch.bfloat16)

@@ -55,6 +55,7 @@ SIGNATURES = {
     "vpf_attention_bf16": [_P, _P, _I64, _I32, _I32, _I32, _F32, _I32, _P],
     "vpf_attention_f32": [_P, _P, _I64, _I32, _I32, _I32, _F32, _I32, _P],
     "vpf_attention_bf16_mx8": [_P, _I64, _I32, _I32, _I32, _F32, _P, _I64, _P, _I64, _P],
+    "vpf_head_gather_bf16": [_P, _I64, _I32, _I32, _P, _I64, _P],
     "vpf_cls_attn_fold_bf16": [_P, _I64, _I32, _I32, _P, _I64, _F32, _P, _I64, _P, _I64, _P, _F32, _P, _I64, _P],
     "vpf_cls_weight_bf16": [_P, _I64, _I32, _I32, _P, _P, _F32, _P, _F32, _I32, _P, _P, _P, _P],
     "vpf_cls_weight_f32": [_P, _I64, _I32, _I32, _P, _P, _F32, _P, _F32, _I32, _P, _P, _P, _P],

@@ -6,8 +6,8 @@
 //   s_hj = q_h . k_hj = LNraw_j . G_h + c0_h,    G_h = W'_k,h^T q_h  (a D-vector),  c0_h = q_h . b'_k,h
 //   o_h  = sum_j p_hj v_hj = W'_v,h U_h + b'_v,h,   U_h = sum_j p_hj LNraw_j,   p_h = softmax_j(s_h * scale)
 // so the K / V GEMMs over all N tokens (2 x 2 N D^2 flops per particle) become one D-long dot and one D-long
-// axpy per (token, head): this kernel. G comes from a block-diagonal GEMM of the CLS queries, and o from a
-// block-diagonal GEMM of U (vit.py).
+// axpy per (token, head): this kernel. G comes from a block-diagonal GEMM of the CLS queries; o from one dense GEMM
+// of the (particle, head) rows of U against W'_v (bias b'_v) whose diagonal blocks k_head_gather copies out (vit.py).
 //
 // One 256-thread workgroup (4 waves) per particle; the particle's N token rows stream through LDS once, in
 // chunks of 16 rows (double-buffered, register-staged: chunk c+2 is loaded while chunk c is consumed), and
@@ -218,7 +218,30 @@ __global__ __launch_bounds__(256) void k_cls_attn_fold(const bf16_t* __restrict_
     }
 }
 
+// out[p][h hd + d] = Y[p H + h][h hd + d]: the diagonal blocks of the dense per-(particle, head) V projection.
+__global__ __launch_bounds__(256) void k_head_gather(const uint4* __restrict__ Y, int64_t n, int H, int hd8,
+                                                     uint4* __restrict__ out, int64_t ldo8) {
+    const int64_t D8 = (int64_t)H * hd8;   // 16-B pieces per row
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * D8) return;
+    const int64_t p = i / D8;
+    const int c = (int)(i - p * D8), h = c / hd8;
+    out[p * ldo8 + c] = Y[(p * H + h) * D8 + c];
+}
+
 }  // namespace
+
+VPF_API int vpf_head_gather_bf16(const uint16_t* Y, int64_t n, int H, int hd, uint16_t* out, int64_t ldo,
+                                 void* stream) {
+    if (n < 0 || H <= 0 || hd <= 0 || hd % 8 != 0 || ldo < (int64_t)H * hd || ldo % 8 != 0 || !Y || !out ||
+        ((uintptr_t)Y & 15) || ((uintptr_t)out & 15))
+        return VPF_ERR_ARG;
+    if (n == 0) return 0;
+    const int64_t work = n * H * (hd / 8);
+    hipLaunchKernelGGL(k_head_gather, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint4*>(Y), n, H, hd / 8, reinterpret_cast<uint4*>(out), ldo / 8);
+    VPF_RETURN_LAUNCH();
+}
 
 VPF_API int vpf_cls_attn_fold_bf16(const uint16_t* tokens, int64_t n_part, int N, int H, const float* planes,
                                    int64_t plane_rows, float eps, const uint16_t* G, int64_t ldg, const uint16_t* q,

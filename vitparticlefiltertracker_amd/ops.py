@@ -384,6 +384,18 @@ def cls_attn_fold_(tokens: torch.Tensor, planes: torch.Tensor, eps: float, G: to
          ptr(q), ldq, ptr(bk), 64 ** -0.5, ptr(out), ldo, stream_ptr())
 
 
+@torch.library.custom_op("vpf::head_gather_", mutates_args={"out"}, device_types="cuda")
+def head_gather_(Y: torch.Tensor, heads: int, out: torch.Tensor) -> None:
+    """out[p][h*hd + d] = Y[p*heads + h][h*hd + d]: the diagonal blocks of a per-(particle, head) projection
+    (vpf_head_gather_bf16). Y bf16 [n*heads][D] contiguous, out [n][D] row-strided."""
+    _dev(Y)
+    _chk(out.is_cuda and Y.dtype == _BF16 and out.dtype == _BF16, "head_gather_: bf16 Y / out")
+    R, D = Y.shape
+    n, ldo = _rows(out, "head_gather_ out")
+    _chk(R == n * heads and out.shape[1] == D and D % heads == 0, "head_gather_: shapes")
+    call("vpf_head_gather_bf16", ptr(Y), n, heads, D // heads, ptr(out), ldo, stream_ptr())
+
+
 @torch.library.custom_op("vpf::cls_weight", mutates_args={"Q", "feat", "sim"}, device_types="cuda")
 def cls_weight(tokens: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, tmpl: torch.Tensor,
                lam: float, bits: int, Q: torch.Tensor, feat: Optional[torch.Tensor],

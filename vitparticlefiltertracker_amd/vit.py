@@ -163,23 +163,22 @@ class ViTEngine:
         self.ng = f32(weights["norm.weight"])
         self.nb = f32(weights["norm.bias"])
         # the last block's CLS attention without K / V (vpf_cls_attn_fold_bf16): LN-folded bf16 with statistics
-        # planes, head dim 64, 6, 12 or 16 heads, N <= 640. Two block-diagonal weights carry the per-head algebra:
-        #   G[p][h D + i] = sum_{k in head h} q[p][k] W'_k[k][i]        (W_G[h D + i][k] = W'_k[k][i])
-        #   x[p][64 h + d] = sum_i W'_v[64 h + d][i] U[p][h D + i] + b'_v (W_V[64 h + d][h D + i] = W'_v[64 h + d][i])
+        # planes, head dim 64, 6, 12 or 16 heads, N <= 640. The per-head algebra:
+        #   G[p][h D + i] = sum_{k in head h} q[p][k] W'_k[k][i]   block-diagonal GEMM (W_G[h D + i][k] = W'_k[k][i])
+        #   x[p][64 h + d] = sum_i W'_v[64 h + d][i] U[p][h D + i] + b'_v[64 h + d]: one dense GEMM of the (p, h)
+        #   rows of U against W'_v, then the diagonal blocks gathered (vpf_head_gather_bf16)
         # VPF_CLS_FUSED=0 keeps the K / V GEMM + attention path (A/B, tests).
         H = A.heads
         self.cls_fused = (self.fold_ln and H in (6, 12, 16) and D == 64 * H and N <= 640
                           and os.environ.get("VPF_CLS_FUSED", "1") != "0")
         if self.cls_fused:
             L = self.layers[-1]
-            Wk, Wv = L["wqkv"][D:2 * D].float(), L["wqkv"][2 * D:].float()
+            Wk = L["wqkv"][D:2 * D].float()
             wg = torch.zeros(H * D, D, device=dev, dtype=torch.float32)
-            wv = torch.zeros(D, H * D, device=dev, dtype=torch.float32)
             for h in range(H):
                 c = slice(64 * h, 64 * h + 64)
                 wg[h * D:(h + 1) * D, c] = Wk[c, :].t()
-                wv[c, h * D:(h + 1) * D] = Wv[c, :]
-            self.w_clsG, self.w_clsV = wg.to(dt).contiguous(), wv.to(dt).contiguous()
+            self.w_clsG = wg.to(dt).contiguous()
             self.b_clsG = torch.zeros(H * D, device=dev, dtype=torch.float32)
         self._alloc(self.batch)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -368,8 +367,10 @@ class ViTEngine:
                     _run(T, "gemm_cls_g", vpf.gemm, qc, self.w_clsG, self.b_clsG, None, None, 0, None, None, BIAS, G)
                     _run(T, "attention_cls", vpf.cls_attn_fold_, self.h[:n], pl, eps, G, qc, L["bqkv"][D:2 * D],
                          A.heads, U)
-                    _run(T, "gemm_cls_v", vpf.gemm, U, self.w_clsV, L["bqkv"][2 * D:], None, None, 0, None, None,
-                         BIAS, xc)
+                    Y = self.clsG[:n].view(n * A.heads, D)   # G's storage: G is consumed by attention_cls
+                    _run(T, "gemm_cls_v", vpf.gemm, U.view(n * A.heads, D), L["wqkv"][2 * D:], L["bqkv"][2 * D:],
+                         None, None, 0, None, None, BIAS, Y)
+                    _run(T, "cls_v_gather", vpf.head_gather_, Y, A.heads, xc)
                 elif self.fp8:
                     s8, p8 = ln_stats8(h2)
                     _run(T, "gemm_kv", vpf.gemm_mx8, h8q, h8s, *L["wkv8"], L["bqkv"][D:], None, s8, L["cqkv8"][D:],
