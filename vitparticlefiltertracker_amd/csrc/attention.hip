@@ -167,6 +167,71 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
         }
 }
 
+// The last key step when at most 8 keys of its 32 are real (N - kb <= 8: N = 197 -> 5 keys, N = 577 -> 1).
+// Lane (l32, hh) holds key offsets (r & 3) + 8 (r >> 2) + 4 hh in s[r], so only r = 0..3 can be real: the
+// max / exp / sum run on those 4 (12 of 16 registers are dead, and only their 4 need the key < N test),
+// the probabilities of keys 8..31 are 0, and the second 16-key PV half (st = 1) is skipped. Padded K / V rows
+// are copies of row N - 1 (finite), so the zero probabilities add exactly nothing, as in attn_step<MASK>.
+__device__ __forceinline__ void attn_step_tail8(const char* Ks, const char* Vs, int kb, int N, int lane,
+                                                const bf16x8 qf[4], float scale_log2, float& m, float& l,
+                                                f32x16& o0, f32x16& o1) {
+    const int l32 = lane & 31, hh = lane >> 5;
+    f32x16 s = f32x16{};
+    const int kr = kb + l32;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s, 0, 0, 0);
+    }
+    float sv[4];
+    float bm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sv[r] = kb + r + 4 * hh < N ? s[r] : -INFINITY;
+        bm = fmaxf(bm, sv[r]);
+    }
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    if (__builtin_expect(__any((bm - m) * scale_log2 > 8.0f), 0)) {
+        const float mn = fmaxf(m, bm);
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            o0[r] *= alpha;
+            o1[r] *= alpha;
+        }
+    }
+    const float msc = m * scale_log2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sv[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], scale_log2, -msc));
+        l += sv[r];
+    }
+    const uint4 u = make_uint4(pack_bf2(sv[0], sv[1]), pack_bf2(sv[2], sv[3]), 0u, 0u);
+    const bf16x8 pf = __builtin_bit_cast(bf16x8, u);
+    const int grp = lane >> 4, gi = lane & 15;
+    const int rq = gi >> 2, cp = gi & 3;
+    bf16x4 vr[2][2];
+    const int rbase = kb + 4 * (grp >> 1) + rq;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
+        const int c16 = col >> 3, inner = (col & 7) * 2;
+        vr[dt][0] = ds_read_tr_asm(Vs, v_off(rbase, c16) + inner);
+        vr[dt][1] = ds_read_tr_asm(Vs, v_off(rbase + 8, c16) + inner);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0]), "+v"(vr[0][1]), "+v"(vr[1][0]), "+v"(vr[1][1])::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const bf16x4 lo = vr[dt][0], hi = vr[dt][1];
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o0, 0, 0, 0);
+        else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o1, 0, 0, 0);
+    }
+}
+
 // One workgroup per (particle, head); one wave per 32-query strip (up to 8 waves, strips beyond loop).
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                    int N, int H, float scale_log2, int q_rows) {
@@ -268,7 +333,7 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 constexpr int PIPE_CPB = 4;
 // OUT8: the output is written as MX8 (the fp8 path's proj A operand) instead of bf16: the same packed bf16
 // values, quantised per 32-dim block (a block = 16 dims of a lane + 16 of its partner half-wave lane).
-template <int CPB, bool OUT8 = false>
+template <int CPB, bool OUT8 = false, bool TAIL8 = true>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_pipe(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows,
     uint8_t* __restrict__ out8 = nullptr, int ld8 = 0, uint8_t* __restrict__ s8 = nullptr, int lds8 = 0) {
@@ -329,7 +394,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             __builtin_amdgcn_s_barrier();
             asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
         }
-        if (active) attn_step<1, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+        if (active) {
+            if (TAIL8 && N - c * 32 <= 8) attn_step_tail8(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+            else attn_step<1, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+        }
     }
     if (!active) return;
     l += __shfl_xor(l, 32, 64);
@@ -567,14 +635,23 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     // whole-image kernel instead (A/B timing); N > 256 always takes it (waves loop over strips).
     const char* mode = getenv("VPF_ATTN_MODE");
     if (N <= 256 && !(mode && mode[0] == '0')) {
+        // VPF_ATTN_TAIL=0: the general masked last step instead of attn_step_tail8 (A/B timing)
+        const char* tail = getenv("VPF_ATTN_TAIL");
+        const bool tail8 = !(tail && tail[0] == '0');
         static bool pipe_attr = false;   // benign race: idempotent attribute set
         if (!pipe_attr) {
-            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB>,
+            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, false, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, false, false>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             pipe_attr = true;
         }
-        hipLaunchKernelGGL(k_attn_bf16_pipe<PIPE_CPB>, dim3((unsigned)(B * H)), dim3(512), lds, (hipStream_t)stream,
-                           qkv, out, N, H, scale_log2, q_rows);
+        if (tail8)
+            hipLaunchKernelGGL((k_attn_bf16_pipe<PIPE_CPB, false, true>), dim3((unsigned)(B * H)), dim3(512), lds,
+                               (hipStream_t)stream, qkv, out, N, H, scale_log2, q_rows);
+        else
+            hipLaunchKernelGGL((k_attn_bf16_pipe<PIPE_CPB, false, false>), dim3((unsigned)(B * H)), dim3(512), lds,
+                               (hipStream_t)stream, qkv, out, N, H, scale_log2, q_rows);
         VPF_RETURN_LAUNCH();
     }
     const int threads = 64 * (strips < 8 ? strips : 8);
