@@ -175,6 +175,9 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
 __device__ __forceinline__ void attn_step_tail8(const char* Ks, const char* Vs, int kb, int N, int lane,
                                                 const bf16x8 qf[4], float scale_log2, float& m, float& l,
                                                 f32x16& o0, f32x16& o1) {
+    // the lane id re-read through asm: its address math then stays inside this (last) step instead of being
+    // hoisted above the key loop, where it held ~40 extra VGPRs and spilled
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
     const int l32 = lane & 31, hh = lane >> 5;
     f32x16 s = f32x16{};
     const int kr = kb + l32;
