@@ -47,6 +47,18 @@ __device__ __forceinline__ bf16x4 ds_read_tr(const char* lds_base, int byte_off)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// max / sum of a value with its partner lane l ^ 32 by one v_permlane32_swap (VALU, no LDS round trip; the
+// __shfl_xor form costs a ds_bpermute, its address VALU and an lgkmcnt wait on the step's critical path).
+// Every lane of the wave must be active.
+__device__ __forceinline__ float xor32_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // One key step of T 32-key tiles (T = 1 or 2) for a 32-query strip: S^T = K Q^T on MFMA, online softmax
 // update of (m, l, O), O^T += V^T P^T with V^T fragments from transposed LDS reads. MASK: this step contains
 // padded keys (only the last step). The O / l rescale is skipped when no query's running max moved in this
@@ -87,7 +99,7 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
             }
             bm = fmaxf(bm, s[t][r]);
         }
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    bm = xor32_max(bm);
     // Lazy rescale (T13): the running max m only moves when some query's tile max exceeds it by more than
     // 8 in the exp2 domain, so probabilities stay <= 2^8 (exact in fp32 accumulation, representable in bf16)
     // and the O / l rescale is skipped on almost every tile. The first tile always sets m (m = -inf).
@@ -193,7 +205,7 @@ __device__ __forceinline__ void attn_step_tail8(const char* Ks, const char* Vs, 
         sv[r] = kb + r + 4 * hh < N ? s[r] : -INFINITY;
         bm = fmaxf(bm, sv[r]);
     }
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    bm = xor32_max(bm);
     if (__builtin_expect(__any((bm - m) * scale_log2 > 8.0f), 0)) {
         const float mn = fmaxf(m, bm);
         const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
@@ -294,7 +306,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         int kb = 0;
         for (; kb < nfull; kb += 32) attn_step<1, false>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
         if (kb < NP) attn_step<1, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
-        l += __shfl_xor(l, 32, 64);
+        l = xor32_sum(l);
         const float inv = 1.0f / l;
         if (q < q_rows) {
             bf16_t* orow = out + (row0 + q) * D + h * HD;
@@ -403,7 +415,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
     }
     if (!active) return;
-    l += __shfl_xor(l, 32, 64);
+    l = xor32_sum(l);
     const float inv = 1.0f / l;
     // Lane (l32, hh) holds dims 8k + 4hh .. +3 of query l32 for the eight 8-dim groups k (o0: k < 4, o1: k >= 4).
     // v_permlane32_swap per pair (k, k+1) gives the lower half-wave dims 8k..8k+7 and the upper half-wave
