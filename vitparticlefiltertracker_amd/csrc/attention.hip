@@ -52,7 +52,9 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // Every lane of the wave must be active.
 __device__ __forceinline__ float xor32_max(float x) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    float y;   // one v_max_f32: fmaxf on bit-cast values adds two NaN-canonicalising v_max (scores are never NaN)
+    asm("v_max_f32 %0, %1, %2" : "=v"(y) : "v"(__uint_as_float(r[0])), "v"(__uint_as_float(r[1])));
+    return y;
 }
 __device__ __forceinline__ float xor32_sum(float x) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -103,7 +105,7 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
     // Lazy rescale (T13): the running max m only moves when some query's tile max exceeds it by more than
     // 8 in the exp2 domain, so probabilities stay <= 2^8 (exact in fp32 accumulation, representable in bf16)
     // and the O / l rescale is skipped on almost every tile. The first tile always sets m (m = -inf).
-    if (__builtin_expect(__any((bm - m) * scale_log2 > 8.0f), 0)) {
+    if (__builtin_expect(__any(bm > m + 8.0f / scale_log2), 0)) {   // loop-invariant threshold: 2 VALU, not 3
         const float mn = fmaxf(m, bm);
         const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
         m = mn;
@@ -206,7 +208,7 @@ __device__ __forceinline__ void attn_step_tail8(const char* Ks, const char* Vs, 
         bm = fmaxf(bm, sv[r]);
     }
     bm = xor32_max(bm);
-    if (__builtin_expect(__any((bm - m) * scale_log2 > 8.0f), 0)) {
+    if (__builtin_expect(__any(bm > m + 8.0f / scale_log2), 0)) {   // loop-invariant threshold: 2 VALU, not 3
         const float mn = fmaxf(m, bm);
         const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
         m = mn;
@@ -442,7 +444,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
         for (int b2 = 0; b2 < 2; ++b2) {
             uint32_t am = max(mx8_amax8(ov[2 * b2]), mx8_amax8(ov[2 * b2 + 1]));
-            am = max(am, (uint32_t)__shfl_xor((int)am, 32, 64));
+            {
+                const auto r = __builtin_amdgcn_permlane32_swap(am, am, false, false);
+                am = max(r[0], r[1]);
+            }
             E[b2] = mx8_block_exp(am);
         }
         if (q < q_rows) {
