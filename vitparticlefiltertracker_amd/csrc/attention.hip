@@ -68,10 +68,13 @@ __device__ __forceinline__ float xor32_sum(float x) {
 // ds_read_b64_tr_b16 as inline asm: hipcc treats the builtin as a possible reader of in-flight LDS-DMA
 // bytes and drains vmcnt(0) before it, which would serialise the key-pipelined kernel on its last chunk.
 // The caller waits lgkmcnt itself (tr_wait) before the MFMA that consumes the result.
-__device__ __forceinline__ bf16x4 ds_read_tr_asm(const char* lds_base, int byte_off) {
+// A constant byte offset goes in the instruction's offset field. V rows r + 8 and r + 16 keep bit 1
+// of r, so v_off(r + 8j, c) = v_off(r, c) + 1024 j: the four row blocks of a key step share one address VGPR
+// per 32-dim column tile instead of one v_add each.
+template <int OFF>
+__device__ __forceinline__ bf16x4 ds_read_tr_asm_o(uint32_t addr) {
     bf16x4 r;
-    const uint32_t a = (uint32_t)(size_t)lds_base + (uint32_t)byte_off;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
     return r;
 }
 
@@ -138,16 +141,16 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
     if constexpr (ASM_TR) {
         static_assert(T == 1, "asm transposed-read path handles one 32-key tile");
         bf16x4 vr[2][2][2];
+        const int rbase = kb + 4 * (grp >> 1) + rq;
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            const int rbase = kb + st * 16 + 4 * (grp >> 1) + rq;
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt) {
-                const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
-                const int c16 = col >> 3, inner = (col & 7) * 2;
-                vr[st][dt][0] = ds_read_tr_asm(Vs, v_off(rbase, c16) + inner);
-                vr[st][dt][1] = ds_read_tr_asm(Vs, v_off(rbase + 8, c16) + inner);
-            }
+        for (int dt = 0; dt < 2; ++dt) {
+            const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
+            const int c16 = col >> 3, inner = (col & 7) * 2;
+            const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, c16) + inner);
+            vr[0][dt][0] = ds_read_tr_asm_o<0>(a);
+            vr[0][dt][1] = ds_read_tr_asm_o<1024>(a);
+            vr[1][dt][0] = ds_read_tr_asm_o<2048>(a);
+            vr[1][dt][1] = ds_read_tr_asm_o<3072>(a);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1]),
                      "+v"(vr[1][0][0]), "+v"(vr[1][0][1]), "+v"(vr[1][1][0]), "+v"(vr[1][1][1])::"memory");
@@ -235,8 +238,9 @@ __device__ __forceinline__ void attn_step_tail8(const char* Ks, const char* Vs, 
     for (int dt = 0; dt < 2; ++dt) {
         const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
         const int c16 = col >> 3, inner = (col & 7) * 2;
-        vr[dt][0] = ds_read_tr_asm(Vs, v_off(rbase, c16) + inner);
-        vr[dt][1] = ds_read_tr_asm(Vs, v_off(rbase + 8, c16) + inner);
+        const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, c16) + inner);
+        vr[dt][0] = ds_read_tr_asm_o<0>(a);
+        vr[dt][1] = ds_read_tr_asm_o<1024>(a);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0]), "+v"(vr[0][1]), "+v"(vr[1][0]), "+v"(vr[1][1])::"memory");
     __builtin_amdgcn_sched_barrier(0);
