@@ -80,6 +80,9 @@ def parse():
                     help="fp8: MX-fp8 QKV / FC1 / FC2 GEMMs (configs[4])")
     ap.add_argument("--frame", default="224x224", help="synthetic source frame HxW (configs[4]: 1080x1920)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1: nccl (= RCCL over xGMI, the product path) or gloo "
+                         "(host-staged; lets several ranks share one GPU to rehearse the multi-rank path)")
     ap.add_argument("--kernel-frames", type=int, default=2, help="eager frames timed per kernel (roofline)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (s); 0 = skip")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity cores)")
@@ -146,10 +149,15 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())     # ranks may share a GPU (rehearsal only)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     if args.particles % world:
         raise SystemExit("--particles must be divisible by the number of ranks")
 
@@ -181,7 +189,7 @@ def main() -> int:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     fps = args.steps / elapsed
@@ -229,7 +237,9 @@ def main() -> int:
         "config": {"workload": f"{args.particles} particles, {args.arch} {args.dtype}, {fh}x{fw} frames, "
                                "full tracking step per frame",
                    "particles": args.particles, "particles_per_gpu": n_loc, "arch": args.arch, "frame": [fh, fw],
-                   "hip_graph": not args.no_graph, "parallelism": f"particle-shard x{world}"},
+                   "hip_graph": not args.no_graph, "parallelism": f"particle-shard x{world}",
+                   **({"dist_backend": "gloo (ranks share a GPU: rehearsal, not a product number)"}
+                      if world > 1 and args.dist_backend == "gloo" else {})},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src,

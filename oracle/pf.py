@@ -139,8 +139,9 @@ def resample(Q: np.ndarray, U: int) -> np.ndarray:
 
 
 def weights_to_Q(sim: np.ndarray, lam: float, bits: int) -> np.ndarray:
-    """SPEC S5 from fp32 cosine similarities: Q = floor(exp(lam*(sim-1)) * 2^bits)."""
+    """SPEC S5 from fp32 cosine similarities: Q = floor(exp(lam*(min(sim, 1)-1)) * 2^bits); a non-finite
+    similarity gets Q = 0 (vpf layernorm.hip k_cls_weight)."""
     sim = np.asarray(sim, np.float32)
-    w = np.array([lib().orc_expf(float(np.float32(np.float32(lam) * (s - np.float32(1.0))))) for s in sim],
-                 dtype=np.float32)
+    w = np.array([lib().orc_expf(float(np.float32(np.float32(lam) * (min(s, np.float32(1.0)) - np.float32(1.0)))))
+                  if np.isfinite(s) else 0.0 for s in sim], dtype=np.float32)
     return np.floor(w.astype(np.float64) * float(2 ** bits)).astype(np.int64)

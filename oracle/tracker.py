@@ -61,7 +61,10 @@ class OracleTracker:
 
     def likelihood(self, feats: np.ndarray) -> np.ndarray:
         f = feats.astype(np.float32)
-        sim = (f @ self.template) / np.linalg.norm(f, axis=1)
+        nrm = np.linalg.norm(f, axis=1)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            sim = np.where(nrm > 0, (f @ self.template) / np.where(nrm > 0, nrm, 1), 0)   # zero row: sim 0
+        sim[~np.isfinite(nrm)] = np.nan                                          # SPEC S5: non-finite -> Q 0
         return pf.weights_to_Q(sim.astype(np.float32), self.lam, self.bits)
 
     def track(self, frame: np.ndarray, Q: Optional[np.ndarray] = None) -> Tuple[float, float, float]:

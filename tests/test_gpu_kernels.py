@@ -254,6 +254,49 @@ def test_patch_and_cls_stats_planes():
     assert torch.all(planes[1:, ~patch_rows] == 0)
 
 
+@pytest.mark.parametrize("case", ["offset", "outliers"])
+def test_gemm_stats_planes_cancellation(case):
+    """The planes consumer takes var = sum(sumsq)/D - mean^2 in one pass (fp32); the row_stats path and the
+    oracle take it in two passes. Residual rows with a large common offset (|mean| = 8 std) or a few
+    large-magnitude channels (ViT's outlier dimensions, 40-60x the rest) must give the same LN-folded GEMM
+    output as the two-pass path within bf16 output rounding (parity there was unpinned)."""
+    torch.manual_seed(21)
+    M, D = 777, 768
+    P = D // 64
+    hf = torch.randn(M, D, device=DEV)
+    if case == "offset":
+        hf = hf + 8.0
+    else:
+        idx = torch.tensor([3, 200, 411, 767], device=DEV)
+        hf[:, idx] = hf[:, idx] * 4 + torch.tensor([60.0, -45.0, 52.0, -40.0], device=DEV)
+    x = (torch.randn(M, D, device=DEV) * 0.7).to(torch.bfloat16)
+    W = (torch.randn(D, D, device=DEV) / D ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(D, device=DEV) * 0.1
+    h = hf.to(torch.bfloat16)
+    planes = torch.empty((P, M, 2), device=DEV)
+    # producer writes h in place as h + x W^T + bias; the planes describe the stored rows
+    vpf().gemm_stats_(x, W, bias, h, None, 0, 2, h, planes)
+    N = 2 * D
+    g = 1 + 0.2 * torch.randn(D, device=DEV)
+    be = 0.1 * torch.randn(D, device=DEV)
+    W2 = torch.randn(N, D, device=DEV) / D ** 0.5
+    b2 = 0.1 * torch.randn(N, device=DEV)
+    Wg = (W2 * g).to(torch.bfloat16)
+    cs = Wg.float().sum(1)
+    out_planes = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    vpf().gemm(h, Wg, b2 + W2 @ be, None, None, 0, planes, cs, 4, out_planes, P, 1e-6)
+    st = torch.empty(M, 2, device=DEV)
+    vpf().row_stats(h, 1e-6, st)
+    out_twopass = torch.empty_like(out_planes)
+    vpf().gemm(h, Wg, b2 + W2 @ be, None, None, 0, st, cs, 4, out_twopass)
+    ref = Fn.layer_norm(h.double(), (D,), g.double(), be.double(), 1e-6) @ W2.double().t() + b2.double()
+    torch.testing.assert_close(out_planes.double(), ref, rtol=2e-2, atol=3e-2)
+    # one-pass vs two-pass statistics: the same output up to a few bf16 ulps (relative Frobenius error)
+    rel = ((out_planes.double() - out_twopass.double()).norm() / out_twopass.double().norm()).item()
+    rel_ref = ((out_twopass.double() - ref).norm() / ref.norm()).item()
+    assert rel < 4e-3 and rel < 2 * rel_ref + 1e-4, (rel, rel_ref)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_gemm_strided_rows(dtype):
     """a / out / residual as row-strided views (the last layer's CLS rows of the token tensor)."""
@@ -501,8 +544,38 @@ def test_cls_weight(dtype):
     assert np.array_equal(Q.cpu().numpy(), q_ref)
     # explicit-feature path (ParticleFilter.update)
     Q2 = torch.empty_like(Q)
-    vpf().cosine_weight(feat, t, 20.0, 40, Q2)
+    vpf().cosine_weight(feat, t, 20.0, 40, Q2, None)
     assert np.array_equal(Q2.cpu().numpy(), q_ref)
+
+
+def test_cosine_weight_edge_rows():
+    """SPEC S5 guards: a feature row parallel to the template (fp32 sim may round above 1) still gets
+    Q <= 2^K; rows with NaN / inf get Q = 0; a zero row gets sim 0; an antiparallel row gets exp(-2 lam).
+    Negative or non-finite lambda is rejected by the C-ABI."""
+    torch.manual_seed(4)
+    D, K = 768, 40
+    t = torch.randn(D, device=DEV)
+    t = t / t.norm()
+    rows = [t * 3.7, t * 1e-3, t, -t, torch.zeros(D, device=DEV), torch.randn(D, device=DEV)]
+    bad = torch.randn(D, device=DEV); bad[5] = float("nan"); rows.append(bad)
+    bad = torch.randn(D, device=DEV); bad[9] = float("inf"); rows.append(bad)
+    for k in range(24):                            # near-parallel rows: rounding can push sim past 1
+        rows.append(t * (0.5 + k) + 1e-7 * torch.randn(D, device=DEV))
+    feat = torch.stack(rows).contiguous()
+    Q = torch.empty(feat.shape[0], device=DEV, dtype=torch.int64)
+    sim = torch.empty(feat.shape[0], device=DEV)
+    vpf().cosine_weight(feat, t, 20.0, K, Q, sim)
+    q = Q.cpu().numpy()
+    assert q.max() <= 2 ** K and q.min() >= 0
+    assert q[6] == 0 and q[7] == 0                 # non-finite rows
+    s_host = sim.cpu().numpy()
+    assert np.isnan(s_host[6]) and np.isnan(s_host[7]) and s_host[4] == 0
+    assert np.array_equal(q, pf.weights_to_Q(sim.cpu().numpy(), 20.0, K))
+    assert q[0] == 2 ** K or q[0] >= 2 ** K - 2 ** 18
+    with pytest.raises(Exception):
+        vpf().cosine_weight(feat, t, -1.0, K, Q, None)
+    with pytest.raises(Exception):
+        vpf().cosine_weight(feat, t, float("inf"), K, Q, None)
 
 
 # ------------------------------------------------------------------ H11/H12

@@ -278,3 +278,30 @@ def test_multitracker_two_targets():
             h, w = tex[k].shape[:2]
             cx, cy = starts[k][0] + vel[k][0] * t + w / 2, starts[k][1] + vel[k][1] * t + h / 2
             assert abs(x - cx) < 16 and abs(y - cy) < 16, (t, k, x, y, cx, cy)
+
+
+def test_tracker_upload_mixed_sources_and_size_change():
+    """Frames may arrive as numpy arrays, pinned host tensors or device tensors in any order: the estimates
+    equal an all-numpy run. A frame of another size afterwards re-bounds predict (particles stay inside the
+    new frame) instead of clamping to the init frame."""
+    from vitparticlefiltertracker_amd import Tracker
+    cfg = _tiny_cfg(128, "bf16")
+    w = make_vit_weights(ARCHS["vit_tiny_patch16_224"], seed=3)
+    clip = synthetic_clip(6)
+    ref = Tracker(cfg, weights=w)
+    ref.init(clip[0], (80, 80, 64, 64))
+    e_ref = [ref.track(f) for f in clip[1:]]
+    tr = Tracker(cfg, weights=w)
+    tr.init(torch.from_numpy(clip[0]).pin_memory(), (80, 80, 64, 64))
+    srcs = [torch.from_numpy(clip[1]).pin_memory(), clip[2], torch.from_numpy(clip[3]).to(DEV), clip[4],
+            torch.from_numpy(clip[5]).pin_memory()]
+    assert [tr.track(f) for f in srcs] == e_ref
+    big = np.random.default_rng(1).integers(0, 256, (300, 400, 3), dtype=np.uint8)
+    big[:224, :224] = clip[5]
+    tr.track(big)
+    assert (tr.pf.height, tr.pf.width) == (300, 400)
+    small = np.ascontiguousarray(clip[5][:100, :120])
+    tr.track(small)
+    assert (tr.pf.height, tr.pf.width) == (100, 120)
+    p = tr.pf.particles.cpu().numpy()
+    assert p[0].max() <= 119 and p[1].max() <= 99 and p.min() >= 0

@@ -115,3 +115,27 @@ def test_config_template_update_range():
     assert load_config({"model": {"dtype": "fp8"}})["model"]["dtype"] == "fp8"
     with pytest.raises(ValueError, match="dtype"):
         load_config({"model": {"dtype": "int4"}})
+
+
+def test_config_rejects_bad_lambda():
+    """SPEC S5: lambda must be finite and >= 0, otherwise w = exp(lam (sim - 1)) can exceed 1 and break the
+    K + ceil(log2 P) <= 62 budget of the exact int64 resample."""
+    from vitparticlefiltertracker_amd.config import load_config
+    from vitparticlefiltertracker_amd.particle_filter import ParticleFilter
+    assert load_config({"likelihood": {"lambda": 0.0}})["likelihood"]["lambda"] == 0.0
+    for bad in (-1.0, float("nan"), float("inf")):
+        with pytest.raises(ValueError, match="lambda"):
+            load_config({"likelihood": {"lambda": bad}})
+        with pytest.raises(ValueError, match="lam"):
+            ParticleFilter(16, lam=bad, device="cpu")
+
+
+def test_oracle_weights_clamp_and_nonfinite():
+    """Oracle side of the SPEC S5 guards: sim > 1 is clamped (Q = 2^K exactly), NaN / inf give Q = 0."""
+    import numpy as np
+    from oracle import pf
+    sim = np.array([1.0, 1.0000001, 1.5, np.nan, np.inf, -np.inf, 0.5, 0.9], np.float32)
+    q = pf.weights_to_Q(sim, 20.0, 40)
+    assert q[0] == q[1] == q[2] == 2 ** 40
+    assert q[3] == q[4] == q[5] == 0
+    assert 0 < q[6] < q[7] < 2 ** 40

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import copy
 import dataclasses
+import math
 import os
 from typing import Any, Dict, Optional
 
@@ -117,6 +118,9 @@ def load_config(cfg: Optional[Any] = None) -> Dict[str, Any]:
         raise ValueError(f"unknown model.arch {arch!r}; known: {sorted(ARCHS)}")
     if out["model"]["dtype"] not in ("bf16", "fp8", "fp32"):
         raise ValueError("model.dtype must be 'bf16', 'fp8' or 'fp32'")
+    lam = float(out["likelihood"]["lambda"])
+    if not (math.isfinite(lam) and lam >= 0.0):
+        raise ValueError("likelihood.lambda must be finite and >= 0 (SPEC S5)")
     if not 0.0 <= float(out["likelihood"]["template_update"]) <= 1.0:
         raise ValueError("likelihood.template_update must be in [0, 1]")
     if out["resample"]["method"] != "systematic":

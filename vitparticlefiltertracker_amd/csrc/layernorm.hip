@@ -128,8 +128,12 @@ __global__ __launch_bounds__(256) void k_cls_weight(const T* __restrict__ tok, i
     dot = wave_sum(dot);
     nn = wave_sum(nn);
     if (lane == 0) {
-        const float sim = nn > 0.f ? dot / sqrtf(nn) : 0.f;
-        const float w = fixed_expf(lam * (sim - 1.0f));
+        // SPEC S5: a cosine is <= 1 in exact arithmetic; clamping the fp32 value there keeps w <= 1 and so
+        // Q_i <= 2^K (the K + ceil(log2 P) <= 62 budget). A zero row has sim 0; a row with a NaN / inf (or
+        // whose squared norm overflows fp32) has sim NaN and zero weight.
+        const bool finite = isfinite(dot) && isfinite(nn);
+        const float sim = !finite ? __builtin_nanf("") : (nn > 0.f ? dot / sqrtf(nn) : 0.f);
+        const float w = finite ? fixed_expf(lam * (fminf(sim, 1.0f) - 1.0f)) : 0.0f;
         Q[p] = (int64_t)floor((double)w * scale);
         if (sim_out) sim_out[p] = sim;
     }
@@ -219,7 +223,8 @@ template <typename T>
 int clsw_launch(const T* tokens, int64_t n, int N, int D, const float* gamma, const float* beta, float eps,
                 const float* tmpl, float lam, int bits, float* feat_out, float* sim_out, int64_t* Q,
                 void* stream) {
-    if (n < 0 || N <= 0 || D <= 0 || D % 4 != 0 || D > 1024 || bits < 0 || bits > 62 || !Q || !tmpl)
+    if (n < 0 || N <= 0 || D <= 0 || D % 4 != 0 || D > 1024 || bits < 0 || bits > 62 || !Q || !tmpl ||
+        !(lam >= 0.f) || !(lam <= 3.0e38f))
         return VPF_ERR_ARG;
     if (n == 0) return 0;
     const unsigned blocks = (unsigned)((n + 3) / 4);

@@ -409,13 +409,15 @@ def cls_weight(tokens: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, ep
          ptr(Q), stream_ptr())
 
 
-@torch.library.custom_op("vpf::cosine_weight", mutates_args={"Q"}, device_types="cuda")
-def cosine_weight(feat: torch.Tensor, tmpl: torch.Tensor, lam: float, bits: int, Q: torch.Tensor) -> None:
-    """H10 alone: Q from explicit fp32 features [n][D] and a unit template."""
-    _dev(feat, tmpl, Q)
+@torch.library.custom_op("vpf::cosine_weight", mutates_args={"Q", "sim"}, device_types="cuda")
+def cosine_weight(feat: torch.Tensor, tmpl: torch.Tensor, lam: float, bits: int, Q: torch.Tensor,
+                  sim: Optional[torch.Tensor]) -> None:
+    """H10 alone: Q from explicit fp32 features [n][D] and a unit template (optionally the fp32 cosines)."""
+    _dev(feat, tmpl, Q, sim)
     n, D = feat.shape
     _chk(feat.dtype == _F32 and Q.dtype == torch.int64 and Q.numel() == n, "cosine_weight: f32[n][D] -> int64[n]")
-    call("vpf_cosine_weight_f32", ptr(feat), n, D, ptr(tmpl), lam, bits, 0, ptr(Q), stream_ptr())
+    _chk(sim is None or (sim.dtype == _F32 and sim.numel() == n), "cosine_weight: sim f32[n]")
+    call("vpf_cosine_weight_f32", ptr(feat), n, D, ptr(tmpl), lam, bits, ptr(sim), ptr(Q), stream_ptr())
 
 
 @torch.library.custom_op("vpf::shard_stats", mutates_args={"out_T", "out_sums"}, device_types="cuda")

@@ -16,6 +16,7 @@ exchange logic). With G = 1 there is no collective.
 """
 from __future__ import annotations
 
+import math
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -66,13 +67,24 @@ def slot_range(offset: int, shard_T: int, T: int, P: int, U: int) -> Tuple[int, 
     return first_at_least(offset), first_at_least(offset + shard_T)
 
 
+def _all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """all_gather_into_tensor on the group's backend. RCCL ("nccl") takes the device tensors directly, on the
+    current stream. gloo (CPU tests; several ranks sharing one GPU) exchanges host copies."""
+    import torch.distributed as dist
+    if inp.is_cuda and dist.get_backend(group) == "gloo":
+        host = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(host, inp.cpu(), group=group)
+        out.copy_(host)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
 def gather_stats(packed: torch.Tensor, world_size: int, group=None) -> List[Tuple[int, float, float, float]]:
     """All-gather each shard's packed int64[4] = {T_r, bits of sum Qx, sum Qy, sum Qs} and decode on the host.
     Works for any device / backend (RCCL on the GPU box, gloo on CPU)."""
     if world_size > 1:
-        import torch.distributed as dist
         allp = torch.empty(world_size * 4, dtype=torch.int64, device=packed.device)
-        dist.all_gather_into_tensor(allp, packed.contiguous().view(-1), group=group)
+        _all_gather_into(allp, packed.contiguous().view(-1), group)
         allp = allp.view(world_size, 4)
     else:
         allp = packed.view(1, 4)
@@ -99,10 +111,9 @@ def plan_resample(stats, P: int, n_local: int, U: int):
 def exchange_chunks(chunk: torch.Tensor, ranges, begin: int, n_local: int, world_size: int, group=None):
     """All-gather the padded per-rank resample chunks ([4][cap] = x, y, s, ancestor bits) and keep the slots
     [begin, begin + n_local) this rank owns. Returns [4][n_local]."""
-    import torch.distributed as dist
     cap = chunk.shape[1]
     allc = torch.empty(world_size * 4 * cap, device=chunk.device, dtype=chunk.dtype)
-    dist.all_gather_into_tensor(allc, chunk.contiguous().view(-1), group=group)
+    _all_gather_into(allc, chunk.contiguous().view(-1), group)
     allc = allc.view(world_size, 4, cap)
     parts = []
     for r, (ra, rb) in enumerate(ranges):
@@ -124,6 +135,8 @@ class ParticleFilter:
             raise ValueError("num_particles must be divisible by world_size")
         if weight_bits + max(1, (num_particles - 1).bit_length()) > 62:
             raise ValueError("weight_bits + ceil(log2 P) must be <= 62 (SPEC S5)")
+        if not (math.isfinite(float(lam)) and float(lam) >= 0.0):
+            raise ValueError("lam must be finite and >= 0 (SPEC S5)")
         self.P = int(num_particles)
         self.rank, self.world_size, self.group = int(rank), int(world_size), group
         self.n_local = self.P // self.world_size
@@ -169,7 +182,7 @@ class ParticleFilter:
         if n != self.n_local:
             raise ValueError(f"update: expected {self.n_local} feature rows, got {n}")
         vpf.cosine_weight(features.to(torch.float32).contiguous(), template.to(torch.float32).contiguous(),
-                          self.lam, self.bits, self.Q)
+                          self.lam, self.bits, self.Q, None)
         self._stats_host = None
         return self.Q
 
@@ -193,9 +206,8 @@ class ParticleFilter:
         if T == 0:
             m = self.particles.to(torch.float64).sum(dim=1)
             if self.world_size > 1:
-                import torch.distributed as dist
                 allm = torch.empty(self.world_size * 3, dtype=torch.float64, device=m.device)
-                dist.all_gather_into_tensor(allm, m.contiguous(), group=self.group)
+                _all_gather_into(allm, m.contiguous(), self.group)
                 m = allm.view(self.world_size, 3).sum(dim=0)
             m = (m / self.P).tolist()
             return float(m[0]), float(m[1]), float(m[2])

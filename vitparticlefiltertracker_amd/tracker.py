@@ -65,6 +65,7 @@ class Tracker:
         self.box_wh: Optional[Tuple[float, float]] = None
         self._frame_dev: Optional[torch.Tensor] = None
         self._frame_host: Optional[torch.Tensor] = None
+        self._h2d_done: Optional[torch.cuda.Event] = None
         self._graph: Optional[torch.cuda.CUDAGraph] = None
         self.frame_index = 0
 
@@ -90,10 +91,22 @@ class Tracker:
             raise ValueError("frame must be uint8[H][W][3]")
         if self._frame_dev is None or tuple(self._frame_dev.shape) != arr.shape:
             self._frame_dev = torch.empty(arr.shape, dtype=torch.uint8, device=self.device)
-            self._frame_host = torch.empty(arr.shape, dtype=torch.uint8).pin_memory()
             self._graph = None
+        # the pinned staging buffer is sized independently: the device frame may have come from a pinned or
+        # device tensor of this shape, which never touches it
+        if self._frame_host is None or tuple(self._frame_host.shape) != arr.shape:
+            # the previous async copy may still read the old buffer: finish it before dropping it
+            if self._frame_host is not None:
+                torch.cuda.current_stream(self.device).synchronize()
+            self._frame_host = torch.empty(arr.shape, dtype=torch.uint8).pin_memory()
+        elif self._h2d_done is not None:
+            # reusing the staging buffer: the last frame's H2D copy must have finished reading it
+            self._h2d_done.synchronize()
         self._frame_host.numpy()[...] = arr
         self._frame_dev.copy_(self._frame_host, non_blocking=True)
+        if self._h2d_done is None:
+            self._h2d_done = torch.cuda.Event()
+        self._h2d_done.record()
         return self._frame_dev
 
     # ------------------------------------------------------------------ H13
@@ -147,7 +160,10 @@ class Tracker:
     def track(self, frame) -> Tuple[float, float, float]:
         if self.pf is None:
             raise RuntimeError("call init(frame, bbox) first")
-        self._upload(frame)
+        fd = self._upload(frame)
+        if (fd.shape[0], fd.shape[1]) != (self.pf.height, self.pf.width):
+            # a frame of another size: predict clamps to the new bounds (the graph was dropped by _upload)
+            self.pf.height, self.pf.width = int(fd.shape[0]), int(fd.shape[1])
         self.frame_index += 1
         self.pf.predict(self.frame_index)
         self.weigh()
@@ -258,9 +274,10 @@ class MultiTracker:
     def track(self, frame) -> List[Tuple[float, float, float]]:
         if not self.pfs:
             raise RuntimeError("call init(frame, bboxes) first")
-        self._upload(frame)
+        fd = self._upload(frame)
         self.frame_index += 1
         for pf in self.pfs:
+            pf.height, pf.width = int(fd.shape[0]), int(fd.shape[1])
             pf.predict(self.frame_index)
         if self.use_graph:
             if self._graph is None:
