@@ -42,7 +42,8 @@ constexpr int AUX_PARTS = 15;
 constexpr int MAX_PARTS = 16;
 constexpr int AUX_BYTES = 2048 + AUX_PARTS * 2048;
 
-template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false, bool ILV = true, bool PIPED_EPI = true>
+template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false, bool ILV = true, bool PIPED_EPI = true,
+          bool PAR = true>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W,
                                                         const float* __restrict__ bias,
@@ -262,7 +263,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     // unlike asm) keeps it from draining vmcnt(0) - and with it the residual loads - at the first LDS access below
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     uint4 res[16];
-    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
+    constexpr bool PIPE = PIPED_EPI && EPI != VPF_EPI_PATCH && !OUT8;
+    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual<PIPE && PAR>(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
     // every wave is done with the operand ring (reused as 8 x 16 KiB images) and the LN combine is visible; a
     // raw barrier, so the residual loads stay in flight across it (no DMA is outstanding after the K loop)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -273,7 +275,218 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         const int region = (wid >> 1) + ((wid >> 1) >= (nk % 3) ? 1 : 0);
         img = smem + region * OPERAND_BYTES + (wid & 1) * 16384;
     }
-    if constexpr (PIPED_EPI && EPI != VPF_EPI_PATCH && !OUT8) {
+    if constexpr (PIPE) {
+        store_wave_tile_pipe<EPI, PAR>(img, aux, acc, wm, wn, m0, n0, lane, res, C, ldc, M, N,
+                                       EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr, stats_rows);
+    } else {
+        float* prod_stats = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) ? stats_out : nullptr;
+        store_wave_tile<EPI, OUT8>(img, aux, acc, wm, wn, m0, n0, lane, res, pos, g2, C, ldc, M, N, prod_stats,
+                                   stats_rows, o8);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Ping-pong main loop (cdna_hip_programming.md §5 "The 256² 8-phase template", T3+T4): same tile, waves and
+// epilogues as k_gemm_bf16, different sync structure.
+//  * A K-tile is cut into four 16 KiB half-tiles, one per quadrant operand of a wave's 128x64 sub-tile:
+//    A0 / A1 = the A rows of quadrant-row mh = 0 / 1 of BOTH wave rows (rows g*128 + mh*64 + r), B0 / B1 = the
+//    W rows of quadrant-column nh = 0 / 1 of all four wave columns (rows wn*64 + nh*32 + r). Slot (buffer, type)
+//    = 16 KiB at ((kt & 1) * 4 + type) * 16 KiB; 128 KiB ring + 32 KiB epilogue operands.
+//  * Four phases per K-tile, one output quadrant (16 MFMAs) each: q0 (mh0,nh0) reads A0 + B0, q1 (mh0,nh1)
+//    reads B1, q2 (mh1,nh1) reads A1, q3 (mh1,nh0) reads nothing (A1, B0 still in registers). Phase body:
+//    [fragment reads | one half-tile DMA (2 pieces per wave) | counted vmcnt] barrier [lgkmcnt(0), 16 MFMAs]
+//    barrier.
+//  * The wave row wm = 1 runs one barrier behind wm = 0 (one extra barrier before the loop, matched by wm = 0
+//    after it): the two waves that share a SIMD alternate, one issuing MFMAs while the other issues its LDS
+//    reads and DMA (ping-pong).
+//  * Half-tiles are consumed in the order n = 4k + {A0, B0, B1, A1} and half-tile n is DMA'd in phase n - 6:
+//    q0 of K-tile t stages B1(t+1), q1 A1(t+1), q2 A0(t+2), q3 B0(t+2). WAR: a slot is re-staged >= 2 phases
+//    after the phase that last read it (the reads of both wave rows are retired by then). RAW: the vmcnt(8) at
+//    the end of the memory part of phase p leaves the 4 youngest half-tiles (n = p+3 .. p+6) in flight and
+//    retires n <= p+2, which phase p+1 reads after one more barrier. q2 needs no wait (q3 reads nothing).
+//  * Past the last K-tile the DMAs re-stage K-tile nk-1 (identical bytes), so every phase is branch-free.
+template <int EPI, bool OUT8 = false>
+__global__ __launch_bounds__(NTHREADS) void k_gemm_pp(const bf16_t* __restrict__ A, int lda,
+                                                      const bf16_t* __restrict__ W,
+                                                      const float* __restrict__ bias,
+                                                      const bf16_t* residual,
+                                                      const float* __restrict__ pos, int g2,
+                                                      const float2* __restrict__ stats,
+                                                      const float* __restrict__ colsum,
+                                                      bf16_t* C, int ldc, int M, int N, int K, int group,
+                                                      int stats_parts, float ln_eps, float* stats_out,
+                                                      int stats_rows, Out8 o8) {
+    constexpr int HALF = 16384;
+    constexpr int RING = 8 * HALF;   // 2 buffers x {A0, B0, B1, A1}
+    static_assert(RING + AUX_BYTES <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char smem[RING + AUX_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 2, wn = wid & 3;
+
+    int m0, n0;
+    tile_of(M, N, group, m0, n0);
+
+    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * lda * 2;
+    const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2;
+    // per-lane DMA source offsets: [type][piece]; piece p of a half-tile = local rows (wid + 8p) * 8 + lane / 8
+    uint32_t off[4][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int rho = (wid + 8 * p) * 8 + (lane >> 3);             // local row 0..127
+        const int lch = (lane & 7) ^ ((rho >> 1) & 7);               // logical chunk at this physical slot
+        const int ra0 = (rho >> 6) * 128 + (rho & 63);               // A0: g*128 + r
+        const int rb0 = (rho >> 5) * 64 + (rho & 31);                // B0: wn*64 + r
+        const int ra[2] = {ra0, ra0 + 64}, rb[2] = {rb0, rb0 + 32};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            off[h == 0 ? 0 : 3][p] = (uint32_t)min(ra[h], M - 1 - m0) * (uint32_t)(lda * 2) + (uint32_t)(lch * 16);
+            off[h == 0 ? 1 : 2][p] = (uint32_t)min(rb[h], N - 1 - n0) * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
+        }
+    }
+    const int nk = K / BK;
+    // type: 0 = A0, 1 = B0, 2 = B1, 3 = A1
+    auto stage = [&](int type, int kt) {
+        kt = min(kt, nk - 1);
+        char* slot = smem + ((kt & 1) * 4 + type) * HALF;
+        const char* src = (type == 0 || type == 3) ? Ablk : Bblk;
+        const uint32_t koff = (uint32_t)kt * (BK * 2);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+            __builtin_amdgcn_global_load_lds((gptr_t)(src + off[type][p] + koff), (lptr_t)(slot + (wid + 8 * p) * 1024),
+                                             16, 0, 0);
+    };
+
+    // epilogue operands (same layout as k_gemm_bf16's aux region), issued first: retired by the prologue wait
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    char* aux = smem + RING;
+    if (wid == 0)
+        __builtin_amdgcn_global_load_lds((gptr_t)(bias + min(n0 + lane * 4, N - 4)), (lptr_t)aux, 16, 0, 0);
+    if constexpr (LN) {
+        if (wid == 1)
+            __builtin_amdgcn_global_load_lds((gptr_t)(colsum + min(n0 + lane * 4, N - 4)), (lptr_t)(aux + 1024), 16, 0, 0);
+        const float* sd = reinterpret_cast<const float*>(stats);
+        const int planes = stats_parts > 0 ? stats_parts : 1;
+        if ((M & 1) == 0 && ((uintptr_t)sd & 15) == 0) {
+            for (int pc = wid; pc < 2 * planes; pc += 8) {
+                const int p = pc >> 1, hf = pc & 1;
+                __builtin_amdgcn_global_load_lds((gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + hf * 256 + lane * 4, 2 * M - 4)),
+                                                 (lptr_t)(aux + 2048 + p * 2048 + hf * 1024), 16, 0, 0);
+            }
+        } else {
+            for (int p = 0; p < planes; ++p)
+                __builtin_amdgcn_global_load_lds((gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + wid * 64 + lane, 2 * M - 1)),
+                                                 (lptr_t)(aux + 2048 + p * 2048 + wid * 256), 4, 0, 0);
+        }
+    }
+    // prologue: half-tiles n = 0..5 (K-tile 0 whole, A0 / B0 of K-tile 1); retire n <= 1 (+ the aux pieces)
+    stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0); stage(0, 1); stage(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();   // the ping-pong offset
+    asm volatile("" ::: "memory");
+
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int fr = lane & 15, fq = lane >> 4;
+    // fragment read byte offsets inside a half-tile slot (without the k-chunk term): A rows wm*64 + i*16 + fr,
+    // B rows wn*32 + j*16 + fr; (row >> 1) & 7 = (fr >> 1) & 7 for every fragment (row bases are multiples of 16)
+    const int sw = (fr >> 1) & 7;
+    const int abase = (wm * 64 + fr) * 128, bbase = (wn * 32 + fr) * 128;
+    auto mfma_quadrant = [&](const i32x4 (&fa)[2][4], const i32x4 (&fb)[2][2], int mh, int nh) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[nh * 2 + j][mh * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8, fb[ks][j]), __builtin_bit_cast(bf16x8, fa[ks][i]),
+                        acc[nh * 2 + j][mh * 4 + i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto read_a = [&](i32x4 (&fa)[2][4], const char* slot) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fa[ks][i] = lds16(slot + abase + i * 2048 + (((ks * 4 + fq) ^ sw) << 4));
+    };
+    auto read_b = [&](i32x4 (&fb)[2][2], const char* slot) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) fb[ks][j] = lds16(slot + bbase + j * 2048 + (((ks * 4 + fq) ^ sw) << 4));
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* buf = smem + (kt & 1) * 4 * HALF;
+        i32x4 fa0[2][4], fa1[2][4], fb0[2][2], fb1[2][2];
+        // q0: (mh0, nh0)
+        read_a(fa0, buf);
+        read_b(fb0, buf + HALF);
+        stage(2, kt + 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        bar();
+        mfma_quadrant(fa0, fb0, 0, 0);
+        bar();
+        // q1: (mh0, nh1)
+        read_b(fb1, buf + 2 * HALF);
+        stage(3, kt + 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        bar();
+        mfma_quadrant(fa0, fb1, 0, 1);
+        bar();
+        // q2: (mh1, nh1)
+        read_a(fa1, buf + 3 * HALF);
+        stage(0, kt + 2);
+        bar();
+        mfma_quadrant(fa1, fb1, 1, 1);
+        bar();
+        // q3: (mh1, nh0)
+        stage(1, kt + 2);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        bar();
+        mfma_quadrant(fa1, fb0, 1, 0);
+        bar();
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();   // matches wm = 1's offset barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped re-stages past the end
+
+    // ---------------- epilogue (k_gemm_bf16's, on the ring's 8 x 16 KiB) ----------------
+    if constexpr (LN) {
+        if (stats_parts > 0 && tid < BM) {
+            float sm = 0.f, sq = 0.f;
+            for (int p = 0; p < stats_parts; ++p) {
+                const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + p * 2048 + tid * 8);
+                sm += st.x;
+                sq += st.y;
+            }
+            const float inv_k = 1.0f / (float)K;
+            const float mean = sm * inv_k;
+            const float var = fmaxf(fmaf(sq, inv_k, -mean * mean), 0.f);
+            *reinterpret_cast<float2*>(aux + 2048 + tid * 8) = make_float2(mean, __builtin_amdgcn_rsqf(var + ln_eps));
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): nothing outstanding (see k_gemm_bf16)
+    uint4 res[16];
+    constexpr bool PIPE = EPI != VPF_EPI_PATCH && !OUT8;
+    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual<PIPE>(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    char* img = smem + wid * 16384;
+    if constexpr (PIPE) {
         store_wave_tile_pipe<EPI>(img, aux, acc, wm, wn, m0, n0, lane, res, C, ldc, M, N,
                                   EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr, stats_rows);
     } else {
@@ -300,6 +513,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
         else if (kern == 4 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
+        else if (kern == 6 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
+        else if (kern == 5 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr)                \
+            hipLaunchKernelGGL((k_gemm_pp<E, false>), grid, block, 0, s, VPF_GEMM_ARGS);                     \
+        else if (kern == 5 && VPF_IS_PROD(E) && o8.q != nullptr)                                             \
+            hipLaunchKernelGGL((k_gemm_pp<E, VPF_IS_PROD(E)>), grid, block, 0, s, VPF_GEMM_ARGS);            \
         else if (VPF_IS_LN(E) && stats_parts > AUX_PARTS)                                                    \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, VPF_IS_LN(E)>), grid, block, 0, s, VPF_GEMM_ARGS);       \
         else if (VPF_IS_PROD(E) && o8.q != nullptr)                                                          \
@@ -315,16 +534,17 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
 }
 
 // GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, refills issued from the MFMA block (product);
-// 2 = the 2-stage ring, 3 = the deep ring with both refills issued right after the barrier (A/B timing).
+// 2 = the 2-stage ring, 3 = the deep ring with both refills issued right after the barrier, 4 = kernel 1 with the
+// two-pass epilogue, 5 = the ping-pong loop k_gemm_pp, 6 = kernel 1 with the original epilogue row order (A/B timing).
 // VPF_GEMM_KERNEL sets the initial value, vpf_gemm_tune() the current one.
 static int g_kernel = -1;
 static int gemm_kernel() {
-    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 4) g_kernel = 1; }
+    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 6) g_kernel = 1; }
     return g_kernel;
 }
 int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
 VPF_API int vpf_gemm_tune(int kernel, int group) {
-    if (kernel < 1 || kernel > 4) return VPF_ERR_ARG;
+    if (kernel < 1 || kernel > 6) return VPF_ERR_ARG;
     g_kernel = kernel;
     if (group >= 0) { tile_group(); g_group = group; }
     return 0;

@@ -148,8 +148,12 @@ __device__ __forceinline__ void epi_to_image(char* img, const char* aux, const f
 // Pipelined form of epi_to_image + store_wave_tile for the epilogues with a bf16 output only (EPI_BIAS / BIAS_GELU /
 // LN / LN_GELU / BIAS_RESIDUAL with its statistics planes): fragment row-group i's math and image rows, then that group's two 16-B store iterations, so
 // the stores start after the first 16 rows instead of after all 128 and drain under the remaining math. Same image
-// layout and store pattern as the two-pass form (bit-identical output).
-template <int EPI>
+// layout as the two-pass form (bit-identical output).
+// PAR: store iteration h of group i covers the group's rows of parity h (rows i*16 + 2*(lane/8) + h; still 8 rows
+// x 128 B per instruction), so the 8-B half swap that the image swizzle applies to odd rows is resolved at compile
+// time instead of by 4 v_cndmask per chunk, and stores / residual loads address from one per-lane base pointer
+// plus a wave-uniform row offset instead of a 64-bit multiply-add each. !PAR: the original row order (A/B, kernel 6).
+template <int EPI, bool PAR = true>
 __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm,
                                                      int wn, int m0, int n0, int lane, const uint4 (&res)[16],
                                                      bf16_t* C, int ldc, int M, int N, float* stats_out,
@@ -157,6 +161,8 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
     constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
     constexpr bool RES = EPI == VPF_EPI_BIAS_RESIDUAL;
     const int fr = lane & 15, fq = lane >> 4, c16 = lane & 7;
+    // PAR: the lane's store pointer at row offset 0 of the wave tile (only dereferenced where ok)
+    bf16_t* Cl = C + (int64_t)(m0 + wm * 128 + 2 * (lane >> 3)) * ldc + (n0 + wn * 64 + c16 * 8);
     float4 bv[4], cv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -197,9 +203,9 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
         __builtin_amdgcn_wave_barrier();   // the image is private to this wave: LDS ops of one wave stay in order
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int row = (2 * i + h) * 8 + (lane >> 3);   // rows of group i only
+            const int row = PAR ? i * 16 + 2 * (lane >> 3) + h : (2 * i + h) * 8 + (lane >> 3);   // rows of group i only
             uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
-            if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+            if (PAR ? (h == 1) : (row & 1) != 0) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
             const int m = m0 + wm * 128 + row;
             const int n = n0 + wn * 64 + c16 * 8;
             const bool ok = m < M && n < N;
@@ -227,7 +233,10 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
                     *reinterpret_cast<float2*>(img + row * 128 + c16 * 8) = make_float2(s1, s2);
                 }
             }
-            if (ok) *reinterpret_cast<uint4*>(C + (int64_t)m * ldc + n) = v;
+            if (ok) {
+                if constexpr (PAR) *reinterpret_cast<uint4*>(Cl + (int64_t)(i * 16 + h) * ldc) = v;
+                else *reinterpret_cast<uint4*>(C + (int64_t)m * ldc + n) = v;
+            }
         }
     }
     if constexpr (RES) {
@@ -253,15 +262,19 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
 // The residual rows a lane adds in store_wave_tile (EPI_BIAS_RESIDUAL): 16 x 16 B, all in flight at once. The
 // kernels issue this right after their K loop, before the epilogue barrier (a raw s_barrier, so the loads stay
 // in flight across it), which gives them the LN combine, the barrier and the image writes to land under.
+// PAR: the row order of store_wave_tile_pipe<EPI, true> (res[2i + h] = row i*16 + 2*(lane/8) + h), from one per-lane
+// base pointer; !PAR: row it*8 + lane/8 (store_wave_tile, store_wave_tile_pipe<EPI, false>).
+template <bool PAR = true>
 __device__ __forceinline__ void load_residual(uint4 (&res)[16], const bf16_t* residual, int wm, int wn, int m0,
                                               int n0, int lane, int ldc, int M, int N) {
     const int c16 = lane & 7;
+    const int n = n0 + wn * 64 + c16 * 8;
+    const bf16_t* rl = residual + (int64_t)(m0 + wm * 128 + (PAR ? 2 : 1) * (lane >> 3)) * ldc + n;
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
-        const int m = m0 + wm * 128 + it * 8 + (lane >> 3);
-        const int n = n0 + wn * 64 + c16 * 8;
-        res[it] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(residual + (int64_t)m * ldc + n)
-                                   : make_uint4(0, 0, 0, 0);
+        const int roff = PAR ? (it >> 1) * 16 + (it & 1) : it * 8;
+        const int m = m0 + wm * 128 + roff + (PAR ? 2 : 1) * (lane >> 3);
+        res[it] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(rl + (int64_t)roff * ldc) : make_uint4(0, 0, 0, 0);
     }
 }
 

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
     // unlike asm) keeps it from draining vmcnt(0) - and with it the residual loads - at the first LDS access below
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     uint4 res[16];
-    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
+    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual<false>(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // raw barrier: the residual loads stay in flight
     __builtin_amdgcn_s_barrier();   // the ring is free: 8 x 16 KiB epilogue images
     asm volatile("" ::: "memory");
