@@ -23,6 +23,7 @@
 //  * Workgroup -> tile mapping is XCD-aware (bijective remap, cdna_hip_programming.md §5 T1): the blocks
 //    that share an XCD walk consecutive tiles of one 256-row A panel, so the panel is an L2 hit.
 #include <stdlib.h>
+#include <type_traits>
 #include "gemm_common.h"
 
 using namespace vpf;
@@ -496,6 +497,251 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_pp(const bf16_t* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Four-wave variant (hipBLASLt's gfx950 shape: 256 threads, each wave a 128 x 128 sub-tile with its 256 fp32
+// accumulators in AGPRs, one wave per SIMD): half the LDS fragment bytes per MFMA of the 8-wave kernel.
+//  * Same 256x256x64 tile, swizzled LDS image, deep ring (A slots 0-2, B slots 3-4) and XCD-aware tile order as
+//    k_gemm_bf16. A K-tile's two 32-deep slices are the two MFMA phases of one loop iteration:
+//      phase A: 64 MFMAs on slice 0 (fragments F0_t in registers), the 16 fragment reads of slice 1 (F1_t)
+//               interleaved one per 4 MFMAs;
+//      lgkmcnt(0), vmcnt(8), ONE barrier Y_t (K-tile t+1 landed for every wave; every wave's reads of K-tile t
+//               are retired);
+//      phase B: 64 MFMAs on slice 1 (F1_t), the 16 reads of K-tile t+1's slice 0 (F0_{t+1}) and the 16 DMA
+//               pieces B(t+2), A(t+3) interleaved. Both refills go to the slots of K-tile t, whose last reads
+//               (F1_t) were retired before Y_t. Lookahead: B one K-tile, A two.
+//  * vmcnt(8) at Y_t leaves A(t+2) (issued last, in phase B of t-1) in flight and retires B(t+1), A(t+1).
+//  * Past the end the refills re-read K-tile nk-1 into its own slots (identical bytes) and the phase-B reads of
+//    K-tile nk read unused bytes, so the loop body is branch-free. The epilogue operands land in A slot nk % 3
+//    (K-tile nk-3's, free after Y_{nk-3}), issued after Y_{nk-2}; the epilogue images use the B slots.
+//  * hipcc does not keep 256 builtin-MFMA accumulators resident in AGPRs (it copies every C operand through
+//    a[0:3]), so the MFMAs, fragment reads and their waits are inline asm (cdna_hip_programming.md §5.7): "+a"
+//    accumulators, lds16 reads retired by explicit lgkmcnt(0) statements that name their registers, the first
+//    slice with C = 0 (no AGPR zero-fill), and the MFMA -> VALU hazard padded before the epilogue reads.
+//  * Epilogue: the 8-wave epilogue functions, once per 64-column half (wn' = 2 wn + h).
+__device__ __forceinline__ void mfma_acc(f32x4& c, const i32x4& w, const i32x4& x) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(x));
+}
+__device__ __forceinline__ void mfma_zero(f32x4& c, const i32x4& w, const i32x4& x) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(w), "v"(x));
+}
+// lgkmcnt(0) that the compiler sees as writing the named fragment registers: no copy of them can be scheduled
+// between their lds16 reads and this wait (§5.7 item 1, form ii)
+#define VPF_W4_WAIT16(A, B)                                                                                          \
+    asm volatile("s_waitcnt lgkmcnt(0)"                                                                          \
+                 : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(A[3]), "+v"(A[4]), "+v"(A[5]), "+v"(A[6]), "+v"(A[7]), \
+                   "+v"(B[0][0]), "+v"(B[0][1]), "+v"(B[0][2]), "+v"(B[0][3]), "+v"(B[1][0]), "+v"(B[1][1]),        \
+                   "+v"(B[1][2]), "+v"(B[1][3])::"memory")
+
+// BAL: A(t+2) is issued in phase A of K-tile t (8 pieces per phase) instead of A(t+3) in phase B; the prologue then
+// stages A0 B0 A1 B1 and the vmcnt count at Y_t is the same (A(t+2), issued after B(t+1)... see phase_a).
+template <int EPI, bool OUT8 = false, bool BAL = true>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, const float* __restrict__ bias,
+               const bf16_t* residual, const float* __restrict__ pos, int g2, const float2* __restrict__ stats,
+               const float* __restrict__ colsum, bf16_t* C, int ldc, int M, int N, int K, int group, int stats_parts,
+               float ln_eps, float* stats_out, int stats_rows, Out8 o8) {
+    __shared__ __attribute__((aligned(16))) char smem[5 * OPERAND_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    int m0, n0;
+    tile_of(M, N, group, m0, n0);
+    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * lda * 2;
+    const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2;
+    uint32_t offA[8], offB[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int row = 8 * (i * 4 + wid) + (lane >> 3);
+        const int lch = (lane & 7) ^ ((row >> 1) & 7);
+        offA[i] = (uint32_t)min(row, M - 1 - m0) * (uint32_t)(lda * 2) + (uint32_t)(lch * 16);
+        offB[i] = (uint32_t)min(row, N - 1 - n0) * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
+    }
+    const int nk = K / BK;
+    auto dma_a = [&](int kt, int i) {
+        __builtin_amdgcn_global_load_lds((gptr_t)(Ablk + offA[i] + (uint32_t)kt * (BK * 2)),
+                                         (lptr_t)(smem + (kt % 3) * OPERAND_BYTES + (i * 4 + wid) * 1024), 16, 0, 0);
+    };
+    auto dma_b = [&](int kt, int i) {
+        __builtin_amdgcn_global_load_lds((gptr_t)(Bblk + offB[i] + (uint32_t)kt * (BK * 2)),
+                                         (lptr_t)(smem + (3 + (kt & 1)) * OPERAND_BYTES + (i * 4 + wid) * 1024), 16, 0,
+                                         0);
+    };
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    char* aux = smem + (nk % 3) * OPERAND_BYTES;
+    auto load_aux = [&]() {   // k_gemm_bf16's aux layout, pieces dealt over 4 waves (<= 8 per wave)
+        if (wid == 0)
+            __builtin_amdgcn_global_load_lds((gptr_t)(bias + min(n0 + lane * 4, N - 4)), (lptr_t)aux, 16, 0, 0);
+        if constexpr (LN) {
+            if (wid == 1)
+                __builtin_amdgcn_global_load_lds((gptr_t)(colsum + min(n0 + lane * 4, N - 4)), (lptr_t)(aux + 1024), 16,
+                                                 0, 0);
+            const float* sd = reinterpret_cast<const float*>(stats);
+            const int planes = stats_parts > 0 ? stats_parts : 1;
+            if ((M & 1) == 0 && ((uintptr_t)sd & 15) == 0) {
+                for (int pc = wid; pc < 2 * planes; pc += 4) {
+                    const int p = pc >> 1, hf = pc & 1;
+                    __builtin_amdgcn_global_load_lds(
+                        (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + hf * 256 + lane * 4, 2 * M - 4)),
+                        (lptr_t)(aux + 2048 + p * 2048 + hf * 1024), 16, 0, 0);
+                }
+            } else {
+                for (int p = 0; p < planes; ++p)
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        __builtin_amdgcn_global_load_lds(
+                            (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + (wid * 2 + q) * 64 + lane, 2 * M - 1)),
+                            (lptr_t)(aux + 2048 + p * 2048 + (wid * 2 + q) * 256), 4, 0, 0);
+            }
+        }
+    };
+
+    // fragment reads: A rows wm*128 + i*16 + fr (i < 8), B (W) rows wn*128 + (h*4 + j)*16 + fr; slice ks = logical
+    // chunk ks*4 + fq of the 128-B row
+    const int fr = lane & 15, fq = lane >> 4;
+    const int sw = (fr >> 1) & 7;
+    const int arow = (wm * 128 + fr) * 128, brow = (wn * 128 + fr) * 128;
+    auto slice_base = [&](int kt, int ks, const char*& la, const char*& lb) {
+        la = smem + (kt % 3) * OPERAND_BYTES + arow + (((ks * 4 + fq) ^ sw) << 4);
+        lb = smem + (3 + (kt & 1)) * OPERAND_BYTES + brow + (((ks * 4 + fq) ^ sw) << 4);
+    };
+    // fragment q (0..15) of a slice: q < 8 -> A fragment q, else B fragment (h, j) = ((q-8) >> 2, (q-8) & 3)
+    auto read_frag = [&](i32x4 (&a)[8], i32x4 (&b)[2][4], const char* la, const char* lb, int q) {
+        if (q < 8) a[q] = lds16(la + q * 2048);
+        else b[(q - 8) >> 2][(q - 8) & 3] = lds16(lb + (q - 8) * 2048);
+    };
+
+    f32x4 acc[2][4][8];
+    i32x4 a0[8], b0[2][4], a1[8], b1[2][4];
+
+    // prologue: A0 B0 A1 B1 A2 (8 pieces each); K-tile 0 landed = all but the 24 youngest pieces
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma_a(0, i);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma_b(0, i);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma_a(min(1, nk - 1), i);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma_b(min(1, nk - 1), i);
+    if constexpr (!BAL) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dma_a(min(2, nk - 1), i);
+    }
+    if (nk == 1) load_aux();   // slot 1: no K-tile uses it
+    if constexpr (BAL) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    {
+        const char *la, *lb;
+        slice_base(0, 0, la, lb);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) read_frag(a0, b0, la, lb, q);
+    }
+
+    // phase A: MFMAs of slice 0 (a0/b0) with slice 1's reads (a1/b1) of K-tile kt interleaved, then the barrier
+    auto phase_a = [&](int kt, auto first) {
+        VPF_W4_WAIT16(a0, b0);
+        const char *la, *lb;
+        slice_base(kt, 1, la, lb);
+        const int ka = min(kt + 2, nk - 1);   // BAL: A(kt+2) -> the slot of K-tile kt-1 (free after Y_{kt-1})
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    if constexpr (decltype(first)::value) mfma_zero(acc[h][j][i], b0[h][j], a0[i]);
+                    else mfma_acc(acc[h][j][i], b0[h][j], a0[i]);
+                    if ((i & 3) == 3) {
+                        const int q = (h * 4 + j) * 2 + (i >> 2);
+                        read_frag(a1, b1, la, lb, q);
+                        if (BAL && (q & 1)) dma_a(ka, q >> 1);
+                    }
+                }
+            }
+        VPF_W4_WAIT16(a1, b1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    // phase B: MFMAs of slice 1 (a1/b1) with K-tile kt+1's slice-0 reads and the B(kt+2), A(kt+3) refills
+    auto phase_b = [&](int kt) {
+        if (kt == nk - 2) load_aux();
+        const char *la, *lb;
+        slice_base(kt + 1, 0, la, lb);
+        const int kb = min(kt + 2, nk - 1), ka = min(kt + 3, nk - 1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    mfma_acc(acc[h][j][i], b1[h][j], a1[i]);
+                    if ((i & 3) == 3) {
+                        const int q = (h * 4 + j) * 2 + (i >> 2);
+                        read_frag(a0, b0, la, lb, q);
+                        if (BAL) { if (q & 1) dma_b(kb, q >> 1); }
+                        else if (q < 8) dma_b(kb, q);
+                        else dma_a(ka, q - 8);
+                    }
+                }
+            }
+    };
+    phase_a(0, std::true_type{});
+    phase_b(0);
+    for (int kt = 1; kt < nk; ++kt) {
+        phase_a(kt, std::false_type{});
+        phase_b(kt);
+    }
+    VPF_W4_WAIT16(a0, b0);   // the unused reads of "K-tile nk"
+    // MFMA -> VALU / v_accvgpr_read hazard (§5.7 item 2: up to 12 wait states); the statements name every
+    // accumulator, so no reader of one is scheduled above them
+    asm volatile("s_nop 7\n\ts_nop 7" : "+a"(acc[0][0][0]), "+a"(acc[0][0][1]), "+a"(acc[0][0][2]), "+a"(acc[0][0][3]),
+                 "+a"(acc[0][0][4]), "+a"(acc[0][0][5]), "+a"(acc[0][0][6]), "+a"(acc[0][0][7]));
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            asm volatile("" : "+a"(acc[h][j][0]), "+a"(acc[h][j][1]), "+a"(acc[h][j][2]), "+a"(acc[h][j][3]),
+                         "+a"(acc[h][j][4]), "+a"(acc[h][j][5]), "+a"(acc[h][j][6]), "+a"(acc[h][j][7]));
+
+    // ---------------- epilogue ----------------
+    if constexpr (LN) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the epilogue operands landed ...
+        __builtin_amdgcn_s_barrier();         // ... for every wave
+        if (stats_parts > 0) {               // tid < 256 = BM: one row per thread
+            float sm = 0.f, sq = 0.f;
+            for (int p = 0; p < stats_parts; ++p) {
+                const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + p * 2048 + tid * 8);
+                sm += st.x;
+                sq += st.y;
+            }
+            const float inv_k = 1.0f / (float)K;
+            const float mean = sm * inv_k;
+            const float var = fmaxf(fmaf(sq, inv_k, -mean * mean), 0.f);
+            *reinterpret_cast<float2*>(aux + 2048 + tid * 8) = make_float2(mean, __builtin_amdgcn_rsqf(var + ln_eps));
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    constexpr bool PIPE = EPI != VPF_EPI_PATCH && !OUT8;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    char* img = smem + 3 * OPERAND_BYTES + wid * 16384;   // B slots: never the aux slot
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint4 res[16];
+        if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual<PIPE>(res, residual, wm, 2 * wn + h, m0, n0, lane, ldc, M, N);
+        if constexpr (PIPE) {
+            store_wave_tile_pipe<EPI>(img, aux, acc[h], wm, 2 * wn + h, m0, n0, lane, res, C, ldc, M, N,
+                                      EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr, stats_rows);
+        } else {
+            float* prod_stats = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) ? stats_out : nullptr;
+            store_wave_tile<EPI, OUT8>(img, aux, acc[h], wm, 2 * wn + h, m0, n0, lane, res, pos, g2, C, ldc, M, N,
+                                       prod_stats, stats_rows, o8);
+        }
+        __builtin_amdgcn_wave_barrier();   // the wave's image is reused by the second half (LDS ops stay in order)
+    }
+}
+
 }  // namespace
 
 #define VPF_IS_LN(E) ((E) == VPF_EPI_LN || (E) == VPF_EPI_LN_GELU)
@@ -513,6 +759,10 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_pp(const bf16_t* __restrict__
             hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
         else if (kern == 4 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
+        else if (kern == 7 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr)                \
+            hipLaunchKernelGGL((k_gemm_w4<E, false>), grid, dim3(256), 0, s, VPF_GEMM_ARGS);                   \
+        else if (kern == 7 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && VPF_IS_PROD(E))                 \
+            hipLaunchKernelGGL((k_gemm_w4<E, VPF_IS_PROD(E)>), grid, dim3(256), 0, s, VPF_GEMM_ARGS);          \
         else if (kern == 6 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
         else if (kern == 5 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr)                \
@@ -535,16 +785,17 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
 
 // GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, refills issued from the MFMA block (product);
 // 2 = the 2-stage ring, 3 = the deep ring with both refills issued right after the barrier, 4 = kernel 1 with the
-// two-pass epilogue, 5 = the ping-pong loop k_gemm_pp, 6 = kernel 1 with the original epilogue row order (A/B timing).
+// two-pass epilogue, 5 = the ping-pong loop k_gemm_pp, 6 = kernel 1 with the original epilogue row order, 7 = the
+// four-wave k_gemm_w4 (A/B timing).
 // VPF_GEMM_KERNEL sets the initial value, vpf_gemm_tune() the current one.
 static int g_kernel = -1;
 static int gemm_kernel() {
-    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 6) g_kernel = 1; }
+    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 7) g_kernel = 1; }
     return g_kernel;
 }
 int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
 VPF_API int vpf_gemm_tune(int kernel, int group) {
-    if (kernel < 1 || kernel > 6) return VPF_ERR_ARG;
+    if (kernel < 1 || kernel > 7) return VPF_ERR_ARG;
     g_kernel = kernel;
     if (group >= 0) { tile_group(); g_group = group; }
     return 0;
