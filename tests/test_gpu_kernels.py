@@ -230,6 +230,52 @@ def test_gemm_stats_planes(M, D):
     torch.testing.assert_close(out.double(), ref, rtol=2e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(777, 768, 768), (1000, 2304, 3072)])
+def test_gemm_kernel_variants_bit_identical(M, N, K):
+    """Every A/B variant of the bf16 GEMM (vpf_gemm_tune kernels 2-7: 2-stage ring, refills after the barrier,
+    two-pass epilogue, ping-pong loop, original epilogue row order, four-wave AGPR loop) accumulates each output
+    over the same K order as the product kernel 1, so all of them give the same bits for every epilogue:
+    bias, bias+GELU, residual with statistics planes, LN fold, LN fold + GELU (12 planes). M is not a multiple
+    of the 256-row tile (edge tiles)."""
+    from vitparticlefiltertracker_amd import _lib
+    L = _lib.lib()
+    torch.manual_seed(M + N + K)
+    P = 12
+    A = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV) * 0.1
+    R = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    colsum = W.float().sum(1).contiguous()
+    planes_in = torch.stack([torch.randn(P, M, device=DEV) * 3.0, torch.rand(P, M, device=DEV) * 60 + 40], 2)
+    planes_in = planes_in.contiguous()
+
+    def run(epi):
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        if epi == 2:
+            out.copy_(R)
+            st = torch.zeros((N + 63) // 64, M, 2, device=DEV)
+            vpf().gemm_stats_(A, W, bias, out, None, 0, 2, out, st)
+            return out, st
+        if epi in (4, 5):
+            vpf().gemm(A, W, bias, None, None, 0, planes_in, colsum, epi, out, P, 1e-6)
+        else:
+            vpf().gemm(A, W, bias, None, None, 0, None, None, epi, out)
+        return out, None
+
+    try:
+        for epi in (0, 1, 2, 4, 5):
+            assert L.vpf_gemm_tune(1, -1) == 0
+            ref, ref_st = run(epi)
+            for k in range(2, 8):
+                assert L.vpf_gemm_tune(k, -1) == 0
+                got, st = run(epi)
+                assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (k, epi)
+                if ref_st is not None:
+                    assert torch.equal(st, ref_st), (k, epi)
+    finally:
+        L.vpf_gemm_tune(1, -1)
+
+
 def test_patch_and_cls_stats_planes():
     """EPI_PATCH + vpf_cls_rows_bf16 together fill the planes of every token row (patch rows by the GEMM, CLS
     rows by cls_rows), matching the stored bf16 token rows."""
