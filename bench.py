@@ -12,7 +12,7 @@ resident in HBM before the timed region. Rank 0 prints ONE JSON line. Extra fiel
   roofline      the dominant kernel (the FC1 GEMM by default: the largest FLOP share) timed by HIP events on
                 its own stream in an eager pass after the timed region: achieved TFLOP/s vs the 2.5 PF dense
                 bf16 MFMA peak (MI355X_MICROARCH.md). traffic = HBM bytes per launch of that kernel from the
-                committed PMC summary profiles/r1_pmc_traffic.json (tools/gpu_session.sh pmc), when taken on
+                newest committed PMC summary profiles/r<N>_pmc_traffic.json (tools/gpu_session.sh pmc), when taken on
                 this workload; else null.
   frame_mfma_frac  whole-frame algorithmic FLOPs (35.126 GFLOP/crop) x fps / peak.
   kernels       per-kernel-type HIP-event averages from the same eager pass.
@@ -36,22 +36,27 @@ PEAK_BF16_TFLOPS = 2500.0     # dense bf16 MFMA, /opt/skills/guides/MI355X_MICRO
 PEAK_FP8_TFLOPS = 5000.0      # dense block-scaled e4m3 MFMA (same table), the fp8 path's GEMMs
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+# newest committed PMC summary first (profiles/r<round>_pmc_traffic.json)
+PMC_TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f"r{r}_pmc_traffic.json") for r in (2, 1)]
 
 
 def pmc_traffic(arch_name: str, n_local: int, kernel: str):
     """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_traffic.py over two
     rocprofv3 passes of this bench: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when it was taken on the
     same workload; otherwise (None, reason)."""
-    try:
-        with open(PMC_TRAFFIC) as f:
-            d = json.load(f)
-        if d.get("arch") != arch_name or int(d.get("particles_per_gpu", -1)) != n_local:
-            return None, "no PMC summary for this workload"
-        k = d["kernels"][kernel]
-        return int(k["traffic_bytes"]), os.path.relpath(PMC_TRAFFIC, ROOT)
-    except (OSError, KeyError, ValueError):
-        return None, "no PMC summary"
+    for path in PMC_TRAFFIC_FILES:
+        if not os.path.exists(path):
+            continue
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            if d.get("arch") != arch_name or int(d.get("particles_per_gpu", -1)) != n_local:
+                return None, "no PMC summary for this workload"
+            k = d["kernels"][kernel]
+            return int(k["traffic_bytes"]), os.path.relpath(path, ROOT)
+        except (OSError, KeyError, ValueError):
+            return None, "no PMC summary"
+    return None, "no PMC summary"
 
 
 # BASELINE.json configs as presets (global particle count, arch, dtype, frame). configs[0] is the reference's
