@@ -233,7 +233,8 @@ def test_gemm_stats_planes(M, D):
 @pytest.mark.parametrize("M,N,K", [(777, 768, 768), (1000, 2304, 3072)])
 def test_gemm_kernel_variants_bit_identical(M, N, K):
     """Every A/B variant of the bf16 GEMM (vpf_gemm_tune kernels 2-7: 2-stage ring, refills after the barrier,
-    two-pass epilogue, ping-pong loop, original epilogue row order, four-wave AGPR loop) accumulates each output
+    two-pass epilogue, ping-pong loop, original epilogue row order, four-wave AGPR loop; 10: staggered start; 13:
+    the persistent kernel for the epilogues without a residual) accumulates each output
     over the same K order as the product kernel 1, so all of them give the same bits for every epilogue:
     bias, bias+GELU, residual with statistics planes, LN fold, LN fold + GELU (12 planes). M is not a multiple
     of the 256-row tile (edge tiles)."""
@@ -266,12 +267,51 @@ def test_gemm_kernel_variants_bit_identical(M, N, K):
         for epi in (0, 1, 2, 4, 5):
             assert L.vpf_gemm_tune(1, -1) == 0
             ref, ref_st = run(epi)
-            for k in range(2, 8):
+            for k in (2, 3, 4, 5, 6, 7, 10, 13):
                 assert L.vpf_gemm_tune(k, -1) == 0
                 got, st = run(epi)
                 assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (k, epi)
                 if ref_st is not None:
                     assert torch.equal(st, ref_st), (k, epi)
+    finally:
+        L.vpf_gemm_tune(1, -1)
+
+
+@pytest.mark.parametrize("M,N,K", [(20000, 1000, 768), (70001, 2304, 128), (806912 // 8, 3072, 768)])
+def test_gemm_persistent_bit_identical(M, N, K):
+    """The persistent kernel (vpf_gemm_tune 13: one workgroup per CU walking its XCD's tiles, the operand stream
+    running on across tiles, the stores of one tile in flight into the next one's K loop) against kernel 1 for
+    every epilogue it takes (bias, bias + GELU, LN fold, LN fold + GELU): bit-identical, with several tiles per
+    workgroup, edge tiles in M and N and the shortest K loop (nk = 2)."""
+    from vitparticlefiltertracker_amd import _lib
+    L = _lib.lib()
+    torch.manual_seed(M + N + K)
+    P = 12
+    A = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV) * 0.1
+    colsum = W.float().sum(1).contiguous()
+    planes_in = torch.stack([torch.randn(P, M, device=DEV) * 3.0, torch.rand(P, M, device=DEV) * 60 + 40], 2)
+    planes_in = planes_in.contiguous()
+
+    def run(epi):
+        out = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+        if epi in (4, 5):
+            vpf().gemm(A, W, bias, None, None, 0, planes_in, colsum, epi, out, P, 1e-6)
+        else:
+            vpf().gemm(A, W, bias, None, None, 0, None, None, epi, out)
+        return out
+
+    try:
+        for epi in (0, 1, 4, 5):
+            assert L.vpf_gemm_tune(1, -1) == 0
+            ref = run(epi)
+            for k in (14, 13, 15):
+                assert L.vpf_gemm_tune(k, -1) == 0
+                got = run(epi)
+                torch.cuda.synchronize()
+                bad = (got.view(torch.int16) != ref.view(torch.int16)).sum().item()
+                assert bad == 0, (k, epi, bad)
     finally:
         L.vpf_gemm_tune(1, -1)
 

@@ -23,6 +23,7 @@
 //  * Workgroup -> tile mapping is XCD-aware (bijective remap, cdna_hip_programming.md §5 T1): the blocks
 //    that share an XCD walk consecutive tiles of one 256-row A panel, so the panel is an L2 hit.
 #include <stdlib.h>
+#include <algorithm>
 #include <type_traits>
 #include "gemm_common.h"
 
@@ -43,8 +44,12 @@ constexpr int AUX_PARTS = 15;
 constexpr int MAX_PARTS = 16;
 constexpr int AUX_BYTES = 2048 + AUX_PARTS * 2048;
 
+// LAB (A/B timing only, vpf_gemm_tune kernels 8 - 12): 1 = the C stores predicated off at run time (all epilogue
+// math, image traffic and residual loads kept), 2 = no epilogue at all (the accumulators kept alive by an empty asm),
+// 3 = kernel 1 with a staggered start: the first workgroup on each CU sleeps phase x nk x ~1000 cycles, phase =
+// (block >> 3) mod 2^(group >> 17), so the CUs' epilogue store bursts fall in different phases of the tile period.
 template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false, bool ILV = true, bool PIPED_EPI = true,
-          bool PAR = true>
+          bool PAR = true, int LAB = 0>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W,
                                                         const float* __restrict__ bias,
@@ -66,7 +71,18 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     int m0, n0;
-    tile_of(M, N, group, m0, n0);   // XCD-aware grouped tile order (gemm_common.h); default group 4
+    tile_of(M, N, LAB ? (group & 0xffff) : group, m0, n0);   // XCD-aware grouped tile order (gemm_common.h)
+    if constexpr (LAB == 3) {   // ~T / nph per phase, T ~ nk x 4600 cycles (one K-tile ~2.3 us incl. the fixed cost)
+        const int lg = group >> 17;
+        if ((int)blockIdx.x < 256) {
+            const int steps = (((int)blockIdx.x >> 3) & ((1 << lg) - 1)) * (K / 64);
+            for (int i = 0; i < steps; ++i) {
+                if (lg == 1) __builtin_amdgcn_s_sleep(36);
+                else if (lg == 2) __builtin_amdgcn_s_sleep(18);
+                else __builtin_amdgcn_s_sleep(9);
+            }
+        }
+    }
 
     // ---- per-lane DMA source offsets (bytes, relative to the block's panel base) ----
     const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * lda * 2;
@@ -237,6 +253,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         }
     }
 
+    if constexpr (LAB == 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(acc[j][i]));
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        return;
+    }
+    if constexpr (LAB == 1) { if (group & 0x10000) C = nullptr; }
     // ---------------- epilogue ----------------
     if constexpr (LN) {
         // statistics planes -> {mean, rstd} once per row (in place over plane 0, which only this thread
@@ -277,13 +302,280 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         img = smem + region * OPERAND_BYTES + (wid & 1) * 16384;
     }
     if constexpr (PIPE) {
-        store_wave_tile_pipe<EPI, PAR>(img, aux, acc, wm, wn, m0, n0, lane, res, C, ldc, M, N,
-                                       EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr, stats_rows);
+        store_wave_tile_pipe<EPI, PAR, LAB == 1>(img, aux, acc, wm, wn, m0, n0, lane, res, C, ldc, M, N,
+                                                 EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr, stats_rows);
     } else {
         float* prod_stats = (EPI == VPF_EPI_BIAS_RESIDUAL || EPI == VPF_EPI_PATCH) ? stats_out : nullptr;
         store_wave_tile<EPI, OUT8>(img, aux, acc, wm, wn, m0, n0, lane, res, pos, g2, C, ldc, M, N, prod_stats,
                                    stats_rows, o8);
     }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Persistent form of k_gemm_bf16 for the epilogues without a residual (QKV: LN, FC1: LN + GELU; BIAS, BIAS_GELU).
+// Measured on kernel 1 (vpf_gemm_tune 8 / 9, profiles/r2_gemm_lab/nostore_ab.txt): its C stores cost QKV 0.29 ms and
+// FC1 0.45 ms per launch (11 %) although they are pipelined with the epilogue math: a workgroup ends only once its
+// stores have completed, and the next one on that CU starts with an empty operand ring. A staggered start of the
+// CUs did not change that (stagger_ab.txt), so the fix is to overlap the stores with the next tile's main loop:
+//  * one workgroup per CU; block b (XCD b & 7) walks its XCD's range of logical tiles with stride gridDim / 8, in the
+//    same grouped order as kernel 1;
+//  * the operand stream runs on across tiles: the ring position of K-tile 0 advances by nk + 1 per tile (A slot
+//    (G + kt) % 3, B slot 3 + (G + kt) & 1; the skipped A position is the epilogue-operand slot). The last K-step
+//    (peeled) DMAs the next tile's A0 into the A slot of K-tile nk - 2; after the epilogue barrier its B0 and A1 go
+//    into the slots of K-tile nk - 1, then the epilogue runs on a 2 KiB-per-wave image (one 16-row group at a time,
+//    store_wave_tile_pipe<IMG16>) in the remaining B slot, and its 16 stores per wave stay in flight into the next
+//    tile's first K-step: that step waits vmcnt(20) (A1 + the stores outstanding), a full tile's store count being
+//    fixed; after an edge tile it waits vmcnt(4). gfx950 has one vmcnt for loads and stores, so the second K-step's
+//    wait includes the stores: they have the epilogue tail and one K-step to drain.
+//  * Outputs are bit-identical to kernel 1 (same MFMA order, same epilogue math).
+// MODE (A/B): 0 = the next tile's first K-step waits vmcnt(4) (the stores included); 1 = vmcnt(20) (A1 and the 16
+// stores outstanding); 2 = B1 is also DMA'd before the epilogue (the image moves to the upper half of the epilogue-
+// operand slot, free once the LN combine has run), so the next tile's first two K-steps wait past the stores.
+template <int EPI, int MODE = 1>
+__global__ __launch_bounds__(NTHREADS) void k_gemm_pt(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W,
+                                                      const float* __restrict__ bias, const float2* __restrict__ stats,
+                                                      const float* __restrict__ colsum, bf16_t* C, int ldc, int M, int N,
+                                                      int K, int group, int stats_parts, float ln_eps) {
+    static_assert(EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU || EPI == VPF_EPI_BIAS || EPI == VPF_EPI_BIAS_GELU,
+                  "residual / patch epilogues use k_gemm_bf16");
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    __shared__ __attribute__((aligned(16))) char smem[5 * OPERAND_BYTES];
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    // The lane id is re-read (opaque asm) at the top of every tile and again before its epilogue, so the per-lane
+    // address math of the K loop and of the epilogue is recomputed where it is used instead of being hoisted out of
+    // the tile loop, where it would stay live across the K loop (~70 spilled VGPRs, whose reloads drain vmcnt).
+    int lane = opaque_lane();
+    const int wm = wid >> 2, wn = wid & 3;
+    const int nk = K / BK;
+    const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    const int xcd = blockIdx.x & 7, stride = gridDim.x >> 3;
+    const int lid_end = xcd_first(tiles, xcd + 1);
+    int lid = xcd_first(tiles, xcd) + (blockIdx.x >> 3);
+    if (lid >= lid_end) return;
+    int m0, n0;
+    tile_of_lid(M, N, group, lid, m0, n0);
+
+    // Operand DMA through buffer resources (buffer_load ... lds): one per operand panel of the current tile (A: of the
+    // next one from the last K-step on), with the panel's valid rows as the range, so rows past M / N read 0
+    // (never stored) instead of clamped addresses, and the per-lane offset is tile-independent: piece i of a K-tile
+    // = rows 64 i + 8 wid + lane / 8, the same swizzled chunk for every i; the row and K offsets go in soffset.
+    __amdgpu_buffer_rsrc_t rsA, rsB;
+    auto setup_a = [&](int tm0) {
+        rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)tm0 * lda), (short)0, min(M - tm0, BM) * lda * 2,
+                                                0x00020000);
+    };
+    auto setup_b = [&](int tn0) {
+        rsB = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)tn0 * K), (short)0, min(N - tn0, BN) * K * 2,
+                                                0x00020000);
+    };
+    uint32_t voffA, voffB;
+    {
+        const int row = 8 * wid + (lane >> 3);
+        const int lch = (lane & 7) ^ ((row >> 1) & 7);
+        voffA = (uint32_t)row * (uint32_t)(lda * 2) + (uint32_t)(lch * 16);
+        voffB = (uint32_t)row * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
+    }
+    auto stage_a = [&](int pos, int kt) {   // A K-tile kt -> A slot pos % 3
+        char* la = smem + (pos % 3) * OPERAND_BYTES;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lptr_t)(la + (i * 8 + wid) * 1024), 16, voffA,
+                                                     i * 64 * lda * 2 + kt * (BK * 2), 0, 0);
+    };
+    auto stage_b = [&](int pos, int kt) {   // B K-tile kt -> B slot pos & 1
+        char* lb = smem + (3 + (pos & 1)) * OPERAND_BYTES;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lptr_t)(lb + (i * 8 + wid) * 1024), 16, voffB,
+                                                     i * 64 * K * 2 + kt * (BK * 2), 0, 0);
+    };
+    // The same DMAs as inline asm for the ones issued at the tile boundary (the next tile's A0, B0, A1): hipcc's
+    // waitcnt pass does not see them, so it does not drain them with a vmcnt(0) before the epilogue's LDS accesses;
+    // the K loop's counted waits and barriers order them (below).
+    auto dma_asm = [&](__amdgpu_buffer_rsrc_t rs, char* slot, uint32_t voff, int soff_base, int row_step) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t l = (uint32_t)(size_t)(lptr_t)(slot + (i * 8 + wid) * 1024);
+            // M0 is compiler-reserved: set, used and restored inside the statement, with the M0 -> LDS-DMA wait
+            // state and the SALU-written-descriptor pad (cdna_hip_programming.md §5.7)
+            uint32_t keep;
+            asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                         "buffer_load_dwordx4 %1, %2, %3 offen lds\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(voff), "s"(rs), "s"(soff_base + i * row_step), "s"(l)
+                         : "memory");
+        }
+    };
+    auto stage_a_asm = [&](int pos, int kt) {
+        dma_asm(rsA, smem + (pos % 3) * OPERAND_BYTES, voffA, kt * (BK * 2), 64 * lda * 2);
+    };
+    auto stage_b_asm = [&](int pos, int kt) {
+        dma_asm(rsB, smem + (3 + (pos & 1)) * OPERAND_BYTES, voffB, kt * (BK * 2), 64 * K * 2);
+    };
+    auto read_frags = [&](const char* la, const char* lb, bf16x8 (&a)[2][8], bf16x8 (&b)[2][4], int lane) {
+        const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = wn * 64 + j * 16 + fr;
+                b[ks][j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + (((ks * 4 + fq) ^ ((row >> 1) & 7)) * 16));
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = wm * 128 + i * 16 + fr;
+                a[ks][i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + (((ks * 4 + fq) ^ ((row >> 1) & 7)) * 16));
+            }
+        }
+    };
+
+    setup_a(m0);
+    setup_b(n0);
+    int G = 0;   // ring position of the current tile's K-tile 0 (mod 6)
+    stage_a(G, 0);
+    stage_b(G, 0);
+    stage_a(G + 1, 1);
+    bool first = true, prev_edge = false;
+    for (;;) {
+        lane = opaque_lane();
+        const int nlid = lid + stride;
+        const bool has_next = nlid < lid_end;
+        int nm0 = m0, nn0 = n0;
+        if (has_next) tile_of_lid(M, N, group, nlid, nm0, nn0);
+        const int Gn = (G + nk + 1) % 6;
+        const bool edge = (m0 + BM > M) || (n0 + BN > N);
+        char* aux = smem + ((G + nk) % 3) * OPERAND_BYTES;
+        auto load_aux = [&]() {
+            if (wid == 0)
+                __builtin_amdgcn_global_load_lds((gptr_t)(bias + min(n0 + lane * 4, N - 4)), (lptr_t)aux, 16, 0, 0);
+            if constexpr (LN) {
+                if (wid == 1)
+                    __builtin_amdgcn_global_load_lds((gptr_t)(colsum + min(n0 + lane * 4, N - 4)), (lptr_t)(aux + 1024),
+                                                     16, 0, 0);
+                const float* sd = reinterpret_cast<const float*>(stats);
+                const int planes = stats_parts > 0 ? stats_parts : 1;
+                if ((M & 1) == 0 && ((uintptr_t)sd & 15) == 0) {
+                    for (int pc = wid; pc < 2 * planes; pc += 8) {
+                        const int p = pc >> 1, hf = pc & 1;
+                        __builtin_amdgcn_global_load_lds(
+                            (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + hf * 256 + lane * 4, 2 * M - 4)),
+                            (lptr_t)(aux + 2048 + p * 2048 + hf * 1024), 16, 0, 0);
+                    }
+                } else {
+                    for (int p = 0; p < planes; ++p)
+                        __builtin_amdgcn_global_load_lds(
+                            (gptr_t)(sd + (int64_t)p * 2 * M + min(2 * m0 + wid * 64 + lane, 2 * M - 1)),
+                            (lptr_t)(aux + 2048 + p * 2048 + wid * 256), 4, 0, 0);
+                }
+            }
+        };
+
+        f32x4 acc[4][8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        // K-steps 0 .. nk-2: kernel 1's step (refills B(kt+1), A(kt+2) from the MFMA block; at kt = nk-2 the A
+        // refill re-reads K-tile nk-1 into its own slot, identical bytes, so the block stays branch-free)
+        for (int kt = 0; kt < nk - 1; ++kt) {
+            if (MODE == 1 && kt == 0 && !first && !prev_edge) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+            else if (MODE == 2 && kt < 2 && !first && !prev_edge) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+            else if (MODE == 2 && kt < 2 && !first) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (kt == nk - 2) load_aux();
+            bf16x8 a[2][8], b[2][4];
+            read_frags(smem + ((G + kt) % 3) * OPERAND_BYTES, smem + (3 + ((G + kt) & 1)) * OPERAND_BYTES, a, b, lane);
+            stage_b(G + kt + 1, kt + 1);
+            stage_a(G + min(kt + 2, nk - 1), min(kt + 2, nk - 1));
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], a[ks][i], acc[j][i], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+        }
+        // K-step nk-1 (peeled): everything outstanding lands (incl. the epilogue operands); the refill is the next
+        // tile's A0 into the A slot of K-tile nk-2 (free after this barrier). Without a next tile it rewrites that
+        // free slot with K-tile 0 of this tile (harmless), keeping the block branch-free.
+        {
+            const int kt = nk - 1;
+            // the builtin form: hipcc's waitcnt pass then knows no DMA is outstanding, and inserts no vmcnt(0) of its
+            // own before the epilogue's LDS accesses (which would also drain the asm DMAs of the next tile)
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            bf16x8 a[2][8], b[2][4];
+            read_frags(smem + ((G + kt) % 3) * OPERAND_BYTES, smem + (3 + ((G + kt) & 1)) * OPERAND_BYTES, a, b, lane);
+            setup_a(nm0);
+            stage_a_asm(Gn, 0);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], a[ks][i], acc[j][i], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+        }
+
+        // ---------------- epilogue ----------------
+        lane = opaque_lane();
+        const int tid = wid * 64 + lane;
+        if constexpr (LN) {
+            if (stats_parts > 0 && tid < BM) {
+                float sm = 0.f, sq = 0.f;
+                for (int p = 0; p < stats_parts; ++p) {
+                    const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + p * 2048 + tid * 8);
+                    sm += st.x;
+                    sq += st.y;
+                }
+                const float inv_k = 1.0f / (float)K;
+                const float mean = sm * inv_k;
+                const float var = fmaxf(fmaf(sq, inv_k, -mean * mean), 0.f);
+                *reinterpret_cast<float2*>(aux + 2048 + tid * 8) = make_float2(mean, __builtin_amdgcn_rsqf(var + ln_eps));
+            }
+        }
+        // every wave is done with K-tile nk-1's slots and the LN combine is visible
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (has_next) {
+            setup_b(nn0);
+            stage_b_asm(Gn, 0);        // B slot of K-tile nk-1
+            stage_a_asm(Gn + 1, 1);    // A slot of K-tile nk-1
+            if (MODE == 2) stage_b_asm(Gn + 1, 1);   // B slot of K-tile nk-2 (K-step 0 re-issues it: same bytes)
+        }
+        asm volatile("" ::: "memory");
+        char* img = MODE == 2 ? aux + 16384 + wid * 2048                                 // planes consumed
+                              : smem + (3 + ((G + nk) & 1)) * OPERAND_BYTES + wid * 2048;   // B slot of K-tile nk-2
+        uint4 res_unused[16];
+        store_wave_tile_pipe<EPI, true, false, true>(img, aux, acc, wm, wn, m0, n0, lane, res_unused, C, ldc, M, N,
+                                                     nullptr, 0);
+        if (!has_next) break;
+        first = false;
+        prev_edge = edge;
+        lid = nlid;
+        m0 = nm0;
+        n0 = nn0;
+        G = Gn;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may outlive the workgroup
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -751,9 +1043,45 @@ void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__
         (int)ldc, m, n, k, group, stats_parts, ln_eps, stats_out, stats_rows, o8
 // fp8 copies are produced by the residual-stream producers only (proj, patch embed): the only bf16 GEMMs
 // whose output an MX8 GEMM reads
+#define VPF_GEMM_PT_OK(E) ((E) == VPF_EPI_LN || (E) == VPF_EPI_LN_GELU || (E) == VPF_EPI_BIAS || (E) == VPF_EPI_BIAS_GELU)
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
-        if (kern == 2)                                                                                       \
+        if constexpr (VPF_GEMM_PT_OK(E)) {                                                                   \
+            if (kern >= 13 && stats_parts <= AUX_PARTS && o8.q == nullptr && k >= 2 * BK) {                  \
+                const unsigned pg = (unsigned)std::min<int64_t>((tiles + 7) & ~7, (int64_t)(gemm_cus() & ~7)); \
+                if (kern == 13)                                                                              \
+                    hipLaunchKernelGGL((k_gemm_pt<VPF_GEMM_PT_OK(E) ? E : VPF_EPI_BIAS>), dim3(pg), block, 0, s, A, \
+                                       (int)lda, W, bias, reinterpret_cast<const float2*>(row_stats), colsum, C, \
+                                       (int)ldc, m, n, k, group, stats_parts, ln_eps);                       \
+                else if (kern == 15)                                                                         \
+                    hipLaunchKernelGGL((k_gemm_pt<VPF_GEMM_PT_OK(E) ? E : VPF_EPI_BIAS, 2>), dim3(pg), block, 0, \
+                                       s, A, (int)lda, W, bias, reinterpret_cast<const float2*>(row_stats), colsum, \
+                                       C, (int)ldc, m, n, k, group, stats_parts, ln_eps);                    \
+                else                                                                                         \
+                    hipLaunchKernelGGL((k_gemm_pt<VPF_GEMM_PT_OK(E) ? E : VPF_EPI_BIAS, 0>), dim3(pg), block, 0, \
+                                       s, A, (int)lda, W, bias, reinterpret_cast<const float2*>(row_stats), colsum, \
+                                       C, (int)ldc, m, n, k, group, stats_parts, ln_eps);                    \
+                break;                                                                                       \
+            }                                                                                                \
+        }                                                                                                    \
+        if (kern >= 8 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                   \
+            if (kern >= 10)                                                                                  \
+                hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 3>), grid, block, 0, s, \
+                                   A, (int)lda, W, bias, residual, pos, patch_rows,                           \
+                                   reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,    \
+                                   group | ((kern == 10 ? 2 : kern == 11 ? 1 : 3) << 17), stats_parts, ln_eps, \
+                                   stats_out, stats_rows, o8);                                                \
+            else if (kern == 8)                                                                              \
+                hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 1>), grid, block, 0, s, \
+                                   A, (int)lda, W, bias, residual, pos, patch_rows,                           \
+                                   reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,    \
+                                   group | 0x10000, stats_parts, ln_eps, stats_out, stats_rows, o8);          \
+            else                                                                                             \
+                hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 2>), grid, block, 0, s, \
+                                   A, (int)lda, W, bias, residual, pos, patch_rows,                           \
+                                   reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,    \
+                                   group | 0x10000, stats_parts, ln_eps, stats_out, stats_rows, o8);          \
+        } else if (kern == 2)                                                                                \
             hipLaunchKernelGGL((k_gemm_bf16<E, false>), grid, block, 0, s, VPF_GEMM_ARGS);                    \
         else if (kern == 3 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
@@ -777,6 +1105,16 @@ void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__
             hipLaunchKernelGGL((k_gemm_bf16<E, true>), grid, block, 0, s, VPF_GEMM_ARGS);                     \
     } while (0)
 
+static int gemm_cus() {   // compute units of the current device (the persistent kernel's grid)
+    static int cached = 0;
+    if (!cached) {
+        int dev = 0, n = 0;
+        cached = (hipGetDevice(&dev) == hipSuccess &&
+                  hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n >= 8) ? n : 256;
+    }
+    return cached;
+}
+
 static int g_group = -1;
 static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size of the tile order (0 = tm-major)
     if (g_group < 0) { const char* e = getenv("VPF_GEMM_GROUP"); g_group = e ? atoi(e) : 4; if (g_group < 0) g_group = 0; }
@@ -786,16 +1124,17 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
 // GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, refills issued from the MFMA block (product);
 // 2 = the 2-stage ring, 3 = the deep ring with both refills issued right after the barrier, 4 = kernel 1 with the
 // two-pass epilogue, 5 = the ping-pong loop k_gemm_pp, 6 = kernel 1 with the original epilogue row order, 7 = the
-// four-wave k_gemm_w4 (A/B timing).
+// four-wave k_gemm_w4, 8 / 9 = kernel 1 without its C stores / without its epilogue (A/B timing; outputs not written), 10 / 11 / 12 = kernel 1
+// with a staggered start in 4 / 2 / 8 phases, 13 = the persistent k_gemm_pt (LN / LN_GELU / BIAS / BIAS_GELU; else 1).
 // VPF_GEMM_KERNEL sets the initial value, vpf_gemm_tune() the current one.
 static int g_kernel = -1;
 static int gemm_kernel() {
-    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 7) g_kernel = 1; }
+    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 15) g_kernel = 1; }
     return g_kernel;
 }
 int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
 VPF_API int vpf_gemm_tune(int kernel, int group) {
-    if (kernel < 1 || kernel > 7) return VPF_ERR_ARG;
+    if (kernel < 1 || kernel > 15) return VPF_ERR_ARG;
     g_kernel = kernel;
     if (group >= 0) { tile_group(); g_group = group; }
     return 0;

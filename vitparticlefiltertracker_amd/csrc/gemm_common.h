@@ -30,6 +30,12 @@ __device__ __forceinline__ int lds4(const void* p) {
     asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lptr_t)p));
     return v;
 }
+// the lane id through an opaque asm: values derived from it cannot be hoisted above the statement
+__device__ __forceinline__ int opaque_lane() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -42,10 +48,8 @@ constexpr int TILE_BYTES = BM * 128;       // one operand K-tile: 256 rows x 128
 // A row-panels with the A panel index running fastest, so the ~32 tiles an XCD has in flight cover ~group A
 // panels x 32/group W panels and both stay in that XCD's L2 (profiles/r1_gemm_lab/group_sweep.txt).
 // group = 0: plain tm-major.
-__device__ __forceinline__ void tile_of(int M, int N, int group, int& m0, int& n0) {
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+// logical tile id -> output tile origin (the grouped order described above)
+__device__ __forceinline__ void tile_of_lid(int M, int N, int group, int lid, int& m0, int& n0) {
     const int tiles_n = (N + BN - 1) / BN;
     int tm, tn;
     if (group > 0) {
@@ -62,6 +66,15 @@ __device__ __forceinline__ void tile_of(int M, int N, int group, int& m0, int& n
     }
     m0 = tm * BM;
     n0 = tn * BN;
+}
+// block bid of nwg -> logical tile id: XCD xcd = bid & 7 owns the contiguous range of ids that starts at xcd_first
+__device__ __forceinline__ int xcd_first(int nwg, int xcd) {
+    const int q = nwg >> 3, r = nwg & 7;
+    return xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+}
+__device__ __forceinline__ void tile_of(int M, int N, int group, int& m0, int& n0) {
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    tile_of_lid(M, N, group, xcd_first(nwg, bid & 7) + (bid >> 3), m0, n0);
 }
 
 // bf16-path GELU, two values at a time: x * sigmoid(x (a + b x^2)) = x / (1 + 2^(x (c1 + c2 x^2))), with (a, b)
@@ -153,13 +166,17 @@ __device__ __forceinline__ void epi_to_image(char* img, const char* aux, const f
 // x 128 B per instruction), so the 8-B half swap that the image swizzle applies to odd rows is resolved at compile
 // time instead of by 4 v_cndmask per chunk, and stores / residual loads address from one per-lane base pointer
 // plus a wave-uniform row offset instead of a 64-bit multiply-add each. !PAR: the original row order (A/B, kernel 6).
-template <int EPI, bool PAR = true>
+// IMG16: the image holds one 16-row group (2 KiB per wave, rows indexed mod 16) instead of the wave's 128 rows: the
+// persistent kernel's epilogue, whose free LDS is the next tile's operand ring. Not with the residual statistics.
+template <int EPI, bool PAR = true, bool CHK = false, bool IMG16 = false>   // CHK: C == nullptr skips the C stores (A/B)
 __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm,
                                                      int wn, int m0, int n0, int lane, const uint4 (&res)[16],
                                                      bf16_t* C, int ldc, int M, int N, float* stats_out,
                                                      int stats_rows) {
     constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
     constexpr bool RES = EPI == VPF_EPI_BIAS_RESIDUAL;
+    static_assert(!(RES && IMG16), "the residual statistics partials need the whole 128-row image");
+    constexpr int RMASK = IMG16 ? 15 : 127;
     const int fr = lane & 15, fq = lane >> 4, c16 = lane & 7;
     // PAR: the lane's store pointer at row offset 0 of the wave tile (only dereferenced where ok)
     bf16_t* Cl = C + (int64_t)(m0 + wm * 128 + 2 * (lane >> 3)) * ldc + (n0 + wn * 64 + c16 * 8);
@@ -197,14 +214,14 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
             }
             const int row = i * 16 + fr;
             const int c8 = (j * 4 + fq) ^ (row & 15);
-            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
+            *reinterpret_cast<uint2*>(img + (row & RMASK) * 128 + c8 * 8) =
                 make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
         }
         __builtin_amdgcn_wave_barrier();   // the image is private to this wave: LDS ops of one wave stay in order
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int row = PAR ? i * 16 + 2 * (lane >> 3) + h : (2 * i + h) * 8 + (lane >> 3);   // rows of group i only
-            uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+            uint4 v = *reinterpret_cast<const uint4*>(img + (row & RMASK) * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
             if (PAR ? (h == 1) : (row & 1) != 0) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
             const int m = m0 + wm * 128 + row;
             const int n = n0 + wn * 64 + c16 * 8;
@@ -233,7 +250,7 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
                     *reinterpret_cast<float2*>(img + row * 128 + c16 * 8) = make_float2(s1, s2);
                 }
             }
-            if (ok) {
+            if (ok && (!CHK || C != nullptr)) {
                 if constexpr (PAR) *reinterpret_cast<uint4*>(Cl + (int64_t)(i * 16 + h) * ldc) = v;
                 else *reinterpret_cast<uint4*>(C + (int64_t)m * ldc + n) = v;
             }
