@@ -267,7 +267,7 @@ def test_gemm_kernel_variants_bit_identical(M, N, K):
         for epi in (0, 1, 2, 4, 5):
             assert L.vpf_gemm_tune(1, -1) == 0
             ref, ref_st = run(epi)
-            for k in (2, 3, 4, 5, 6, 7, 10, 13):
+            for k in (2, 3, 4, 5, 6, 7, 10, 13, 16):
                 assert L.vpf_gemm_tune(k, -1) == 0
                 got, st = run(epi)
                 assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (k, epi)

@@ -110,19 +110,42 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             __builtin_amdgcn_global_load_lds((gptr_t)(Bblk + offB[i] + koff), (lptr_t)(lb + g * 1024), 16, 0, 0);
         }
     };
+    // LAB 4: the operand DMAs through per-panel buffer resources (k_gemm_pt's form: one tile-independent VGPR offset per
+    // operand, rows past M / N read 0 and are never stored)
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, min(M - m0, BM) * lda * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * K), (short)0, min(N - n0, BN) * K * 2, 0x00020000);
+    uint32_t voffA = 0, voffB = 0;
+    if constexpr (LAB == 4) {
+        const int row = 8 * wid + (lane >> 3);
+        const int lch = (lane & 7) ^ ((row >> 1) & 7);
+        voffA = (uint32_t)row * (uint32_t)(lda * 2) + (uint32_t)(lch * 16);
+        voffB = (uint32_t)row * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
+    }
     auto stage_a = [&](int kt) {   // DEEP: A K-tile kt -> A slot kt % 3
         char* la = smem + (kt % 3) * OPERAND_BYTES;
         const uint32_t koff = (uint32_t)kt * (BK * 2);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds((gptr_t)(Ablk + offA[i] + koff), (lptr_t)(la + (i * 8 + wid) * 1024), 16, 0, 0);
+        for (int i = 0; i < 4; ++i) {
+            if constexpr (LAB == 4)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lptr_t)(la + (i * 8 + wid) * 1024), 16, voffA,
+                                                         i * 64 * lda * 2 + (int)koff, 0, 0);
+            else
+                __builtin_amdgcn_global_load_lds((gptr_t)(Ablk + offA[i] + koff), (lptr_t)(la + (i * 8 + wid) * 1024), 16, 0, 0);
+        }
     };
     auto stage_b = [&](int kt) {   // DEEP: B K-tile kt -> B slot kt & 1
         char* lb = smem + (3 + (kt & 1)) * OPERAND_BYTES;
         const uint32_t koff = (uint32_t)kt * (BK * 2);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds((gptr_t)(Bblk + offB[i] + koff), (lptr_t)(lb + (i * 8 + wid) * 1024), 16, 0, 0);
+        for (int i = 0; i < 4; ++i) {
+            if constexpr (LAB == 4)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lptr_t)(lb + (i * 8 + wid) * 1024), 16, voffB,
+                                                         i * 64 * K * 2 + (int)koff, 0, 0);
+            else
+                __builtin_amdgcn_global_load_lds((gptr_t)(Bblk + offB[i] + koff), (lptr_t)(lb + (i * 8 + wid) * 1024), 16, 0, 0);
+        }
     };
 
     const int wm = wid >> 2, wn = wid & 3;
@@ -1047,7 +1070,7 @@ void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
         if constexpr (VPF_GEMM_PT_OK(E)) {                                                                   \
-            if (kern >= 13 && stats_parts <= AUX_PARTS && o8.q == nullptr && k >= 2 * BK) {                  \
+            if (kern >= 13 && kern <= 15 && stats_parts <= AUX_PARTS && o8.q == nullptr && k >= 2 * BK) {     \
                 const unsigned pg = (unsigned)std::min<int64_t>((tiles + 7) & ~7, (int64_t)(gemm_cus() & ~7)); \
                 if (kern == 13)                                                                              \
                     hipLaunchKernelGGL((k_gemm_pt<VPF_GEMM_PT_OK(E) ? E : VPF_EPI_BIAS>), dim3(pg), block, 0, s, A, \
@@ -1064,7 +1087,10 @@ void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__
                 break;                                                                                       \
             }                                                                                                \
         }                                                                                                    \
-        if (kern >= 8 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                   \
+        if (kern == 16 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                  \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 4>), grid, block, 0, s,   \
+                               VPF_GEMM_ARGS);                                                               \
+        } else if (kern >= 8 && kern <= 12 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) { \
             if (kern >= 10)                                                                                  \
                 hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 3>), grid, block, 0, s, \
                                    A, (int)lda, W, bias, residual, pos, patch_rows,                           \
@@ -1129,12 +1155,12 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
 // VPF_GEMM_KERNEL sets the initial value, vpf_gemm_tune() the current one.
 static int g_kernel = -1;
 static int gemm_kernel() {
-    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 15) g_kernel = 1; }
+    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 16) g_kernel = 1; }
     return g_kernel;
 }
 int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
 VPF_API int vpf_gemm_tune(int kernel, int group) {
-    if (kernel < 1 || kernel > 15) return VPF_ERR_ARG;
+    if (kernel < 1 || kernel > 16) return VPF_ERR_ARG;
     g_kernel = kernel;
     if (group >= 0) { tile_group(); g_group = group; }
     return 0;

@@ -143,7 +143,9 @@ class Tracker:
             self._features_to_weights()   # warm-up outside capture
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: RCCL's watchdog thread queries events while a capture runs (multi-GPU); "global" would
+        # invalidate the capture on that, the capture itself only involves this thread's stream
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._features_to_weights()
         self._graph = g
 
@@ -267,7 +269,9 @@ class MultiTracker:
             self._forward()
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: RCCL's watchdog thread queries events while a capture runs (multi-GPU); "global" would
+        # invalidate the capture on that, the capture itself only involves this thread's stream
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._forward()
         self._graph = g
 
