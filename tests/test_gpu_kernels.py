@@ -46,8 +46,11 @@ def test_predict_bit_exact(n, begin):
 
 
 # ------------------------------------------------------------------ H2/H3 crop
+@pytest.mark.parametrize("box", [(64.0, 48.0), (300.0, 200.0)])
 @pytest.mark.parametrize("S,patch,H,W", [(224, 16, 224, 224), (336, 14, 240, 320), (224, 16, 1080, 1920)])
-def test_crop_bit_exact(S, patch, H, W):
+def test_crop_bit_exact(S, patch, H, W, box):
+    """Bit-exact against the oracle. patch 16 takes the LDS-staged kernel (one workgroup per particle, its source
+    window in LDS); the (300, 200) box at scale 2 overflows the LDS window and takes its global-tap branch."""
     rng = np.random.default_rng(S + H)
     frame = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
     n = 5
@@ -56,7 +59,6 @@ def test_crop_bit_exact(S, patch, H, W):
     p[1] = [H / 2, 5.5, H - 1.0, 101.3, -40.0]
     p[2] = [1.0, 0.5, 2.0, 1.37, 1.0]
     kp = (3 * patch * patch + 63) // 64 * 64
-    box = (64.0, 48.0)
     ref = pf.crop_patches(frame, p, box, S, patch, kp, (0.5, 0.4, 0.3), (0.5, 0.25, 0.2))
     from vitparticlefiltertracker_amd.vit import norm_affine
     ab = norm_affine((0.5, 0.4, 0.3), (0.5, 0.25, 0.2))

@@ -7,6 +7,8 @@
 // Arithmetic order is SPEC S3's, contraction off, so the fp32 values are bit-identical to
 // oracle/pf_oracle.c and the bf16 values are their RNE rounding.
 #pragma clang fp contract(off)
+#include <cstdlib>
+
 #include "vpf_common.h"
 #include "../../include/vpf.h"
 
@@ -161,6 +163,91 @@ __global__ __launch_bounds__(256) void k_crop_patches_fast(const uint32_t* __res
     }
 }
 
+// LDS-staged form of the fast path: one 512-thread workgroup per particle. The particle's source window (every
+// bilinear tap of its S x S samples, clamped into the zero border as rgba_tap does) is copied from the RGBA workspace
+// into LDS once, and the taps read LDS instead of issuing 32 gathered dword loads per thread through the vector
+// memory path, which bound the global form (the im2col stores are the same). A window larger than CROP_LDS_DW dwords
+// (a large template at a large scale) takes the global taps. Same values and arithmetic as k_crop_patches_fast.
+constexpr int CROP_LDS_DW = 20480;   // 80 KiB: two workgroups per CU; a 64 x 64 template at scale 2 needs 130 x 130
+template <typename OutT>
+__global__ __launch_bounds__(512) void k_crop_patches_lds(const uint32_t* __restrict__ rgba, int H, int W,
+                                                          const float* __restrict__ xs, const float* __restrict__ ys,
+                                                          const float* __restrict__ ss, int n_patches, int g, float w0,
+                                                          float h0, int S, int patch, NormAB nab,
+                                                          OutT* __restrict__ out) {
+    __shared__ uint32_t win[CROP_LDS_DW];
+    const int64_t p = blockIdx.x;
+    const float s = ss[p];
+    const float bw = s * w0, bh = s * h0;
+    const float x0 = xs[p] - 0.5f * bw, y0 = ys[p] - 0.5f * bh;
+    const float dx = bw / (float)S, dy = bh / (float)S;
+    // tap range: the sample coordinate is monotone in the output index, so the first and last samples bound it
+    const int ix_lo = (int)floorf((x0 + (0.0f + 0.5f) * dx) - 0.5f);
+    const int ix_hi = (int)floorf((x0 + ((float)(S - 1) + 0.5f) * dx) - 0.5f) + 1;
+    const int iy_lo = (int)floorf((y0 + (0.0f + 0.5f) * dy) - 0.5f);
+    const int iy_hi = (int)floorf((y0 + ((float)(S - 1) + 0.5f) * dy) - 0.5f) + 1;
+    const int cx0 = min(max(ix_lo, -1), W), cx1 = min(max(ix_hi, -1), W);
+    const int cy0 = min(max(iy_lo, -1), H), cy1 = min(max(iy_hi, -1), H);
+    const int wx = cx1 - cx0 + 1, wy = cy1 - cy0 + 1;
+    const bool staged = wx * wy <= CROP_LDS_DW;   // workgroup-uniform
+    if (staged) {
+        for (int i = threadIdx.x; i < wx * wy; i += 512) {
+            const int r = i / wx, c = i - r * wx;
+            win[i] = rgba[(int64_t)(cy0 + r + 1) * (W + 2) + (cx0 + c + 1)];
+        }
+    }
+    __syncthreads();
+    auto tap = [&](int yy, int xx) -> uint32_t {
+        if (staged) return win[(min(max(yy, -1), H) - cy0) * wx + (min(max(xx, -1), W) - cx0)];
+        return rgba_tap(rgba, H, W, yy, xx);
+    };
+    const int per_row = patch * (patch >> 3);             // threads per im2col row
+    const int pp = patch * patch;
+    for (int t = threadIdx.x; t < n_patches * per_row; t += 512) {
+        const int pi = t / per_row;
+        const int tt = t - pi * per_row;
+        const int ky = tt / (patch >> 3), kx0 = (tt - ky * (patch >> 3)) * 8;
+        const int py = pi / g, px = pi - (pi / g) * g;
+        const int oy = py * patch + ky;
+        const float sy = (y0 + ((float)oy + 0.5f) * dy) - 0.5f;
+        const float fy0 = floorf(sy);
+        const float fy = sy - fy0;
+        const int iy = (int)fy0;
+        float vals[3][8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int ox = px * patch + kx0 + e;
+            const float sx = (x0 + ((float)ox + 0.5f) * dx) - 0.5f;
+            const float fx0 = floorf(sx);
+            const float fx = sx - fx0;
+            const int ix = (int)fx0;
+            const uint32_t t00 = tap(iy, ix), t01 = tap(iy, ix + 1);
+            const uint32_t t10 = tap(iy + 1, ix), t11 = tap(iy + 1, ix + 1);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float top = (1.0f - fx) * chan(t00, c) + fx * chan(t01, c);
+                const float bot = (1.0f - fx) * chan(t10, c) + fx * chan(t11, c);
+                const float v = (1.0f - fy) * top + fy * bot;
+                vals[c][e] = fmaf(v, nab.a[c], nab.b[c]);
+            }
+        }
+        const int64_t row = p * n_patches + pi;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            OutT* dst = out + row * (int64_t)(3 * pp) + c * pp + ky * patch + kx0;
+            if constexpr (sizeof(OutT) == 2) {
+                uint4 pk;
+                pk.x = pack_bf2(vals[c][0], vals[c][1]); pk.y = pack_bf2(vals[c][2], vals[c][3]);
+                pk.z = pack_bf2(vals[c][4], vals[c][5]); pk.w = pack_bf2(vals[c][6], vals[c][7]);
+                *reinterpret_cast<uint4*>(dst) = pk;
+            } else {
+                *reinterpret_cast<float4*>(dst) = make_float4(vals[c][0], vals[c][1], vals[c][2], vals[c][3]);
+                *reinterpret_cast<float4*>(dst + 4) = make_float4(vals[c][4], vals[c][5], vals[c][6], vals[c][7]);
+            }
+        }
+    }
+}
+
 template <typename OutT>
 static int crop_launch(const uint8_t* frame, int H, int W, uint32_t* rgba_ws, const float* particles, int64_t ld,
                        int64_t n, float w0, float h0, int S, int patch, int Kp, const float* norm_ab_host, OutT* out,
@@ -177,7 +264,13 @@ static int crop_launch(const uint8_t* frame, int H, int W, uint32_t* rgba_ws, co
     hipLaunchKernelGGL(k_frame_rgba, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, frame, H, W, rgba_ws);
     const int g = S / patch;
     const int64_t rows = n * g * g;
-    if (patch % 8 == 0 && Kp == 3 * patch * patch) {
+    // VPF_CROP_LDS=0: the global-tap kernel for the fast path (A/B timing)
+    const char* lds_env = getenv("VPF_CROP_LDS");
+    const bool use_lds = !(lds_env && lds_env[0] == '0');
+    if (patch % 8 == 0 && Kp == 3 * patch * patch && use_lds && n <= INT32_MAX) {
+        hipLaunchKernelGGL(k_crop_patches_lds<OutT>, dim3((unsigned)n), dim3(512), 0, st, rgba_ws, H, W, particles,
+                           particles + ld, particles + 2 * ld, g * g, g, w0, h0, S, patch, nab, out);
+    } else if (patch % 8 == 0 && Kp == 3 * patch * patch) {
         const int64_t work = rows * (patch * (patch / 8));
         hipLaunchKernelGGL(k_crop_patches_fast<OutT>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, rgba_ws,
                            H, W, particles, particles + ld, particles + 2 * ld, rows, g * g, g, w0, h0, S, patch, nab,
