@@ -1,0 +1,5 @@
+set -o pipefail
+bash tools/gpu_session.sh r2s4_v1 tests smoke bench || exit $?
+mkdir -p gpurun_out/r2s4_v1
+timeout -k 10 300 python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --particles 512 > gpurun_out/r2s4_v1/bench_p512.log 2>&1 || exit $?
+tail -1 gpurun_out/r2s4_v1/bench_p512.log | cut -c1-300
