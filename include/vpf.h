@@ -190,6 +190,23 @@ int vpf_resample(const int64_t* Q, int64_t n_local, int64_t global_begin, int64_
                  int64_t slot_end, const float* particles, int64_t ld, int32_t* anc_out,
                  float* states_out, int64_t out_ld, int64_t* cdf_ws, void* stream);
 
+/* H11 + H12 over the GLOBAL particle set, device-resident (the product path of ParticleFilter): every rank
+ * holds all P weights and states — its own arrays (world 1: one shard, n_shard = P) or the all-gathered shard
+ * chunks (world > 1) — so nothing goes back to the host between the weights and the resample.
+ * Global index i is shard r = i / n_shard, k = i % n_shard: Q_i = Q[r*q_stride + k] (int64),
+ * (x, y, s)_i = particles[r*p_stride + k + {0, ld, 2*ld}] (fp32).
+ * stats_out: int64[4] = {T = sum Q, then the bits of the fp64 sums sum Q*x, Q*y, Q*s} (SPEC S6, fixed-order tree
+ * over the global index, so every rank and every world size gets the same bits; when T == 0 the sums are taken
+ * with every Q_i = 1 and the estimate is sum / P). cdf_ws: int64[P] workspace (the inclusive CDF).
+ * Resample (SPEC S7, uniform when T == 0) of the output slots [slot_begin, slot_end): anc_out = global ancestor
+ * index, states_out[3][out_ld] its state. The resample word U = Philox(ctr = (0, frame, 1, 0), key = seed) word 0
+ * is drawn on the device (SPEC S1). Requires 0 < P < 2^31, P % n_shard == 0, ld >= n_shard, and for several
+ * shards q_stride >= n_shard, p_stride >= 2*ld + n_shard. Two launches (one workgroup, then one thread per slot). */
+int vpf_estimate_resample(const int64_t* Q, int64_t q_stride, const float* particles, int64_t ld,
+                          int64_t p_stride, int64_t n_shard, int64_t P, uint64_t seed, uint32_t frame,
+                          int64_t slot_begin, int64_t slot_end, int32_t* anc_out, float* states_out,
+                          int64_t out_ld, int64_t* cdf_ws, int64_t* stats_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,7 +1,8 @@
-"""CPU, world_size 2 and 8 (gloo): the multi-rank exchange of ParticleFilter — statistics all-gather, exact
-resample plan, chunk all-gather and slot ownership — reproduces the single-process oracle bit for bit
-(SURVEY.md §8e). The per-shard device work (vpf_shard_stats / vpf_resample) is emulated by the oracle here;
-the GPU tests cover those kernels against the same oracle."""
+"""CPU, world_size 2 and 8 (gloo): the multi-rank exchange of ParticleFilter — each rank's shard chunk (Q int64 |
+x | y | s fp32, `shard_views`) all-gathered as one fixed-size tensor, and the strided global view
+(`global_view`) that vpf_estimate_resample reads — reproduces the single-process oracle bit for bit
+(SURVEY.md §8e). The device call itself is emulated by the oracle over the global arrays read THROUGH the view's
+strides; the GPU tests cover vpf_estimate_resample against the same oracle with the same layout."""
 import os
 import socket
 
@@ -36,62 +37,67 @@ def _worker(rank, world, port, P, seed, frames, q):
         dist.destroy_process_group()
 
 
+def _read_global(view, P):
+    """The global (Q, particles) as vpf_estimate_resample addresses them: index i -> shard r = i // n_shard,
+    k = i % n_shard; Q at r*q_stride + k, x at r*p_stride + k, y / s at + ld / + 2 ld."""
+    Qv, qs, Pv, ld, ps, nsh = view
+    Qn, Pn = Qv.numpy(), Pv.numpy()
+    i = np.arange(P)
+    r, k = i // nsh, i % nsh
+    parts = np.stack([Pn[r * ps + k + c * ld] for c in range(3)])
+    return Qn[r * qs + k].copy(), np.ascontiguousarray(parts)
+
+
 def _body(rank, world, P, seed, frames, q):
-    if True:
-        rng = np.random.default_rng(seed)
-        n = P // world
-        begin = rank * n
-        parts = np.empty((3, P), np.float32)
-        parts[0], parts[1], parts[2] = 100.0, 90.0, 1.0
-        ref = parts.copy()
-        local = np.ascontiguousarray(parts[:, begin:begin + n])
-        results = []
-        for k in range(1, frames + 1):
-            # identical global weights on every rank; each rank uses only its shard
-            Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
-            if k == 2:
-                Q[:] = 0                                  # T == 0 -> uniform fallback path
-            if k == 3:
-                Q[rng.random(P) < 0.9] = 0
-            pf.predict(local, begin, 77, k, (3.0, 3.0, 0.05), 224, 224, (0.5, 2.0))
-            pf.predict(ref, 0, 77, k, (3.0, 3.0, 0.05), 224, 224, (0.5, 2.0))
-            Ql = np.ascontiguousarray(Q[begin:begin + n])
-            T_r, sums = pf.shard_stats(Ql, local)
-            packed = torch.cat([torch.tensor([T_r], dtype=torch.int64),
-                                torch.from_numpy(sums.copy()).view(torch.int64)])
-            stats = PF.gather_stats(packed, world)
-            T = sum(s[0] for s in stats)
-            est = (sum(s[1] for s in stats) / T, sum(s[2] for s in stats) / T, sum(s[3] for s in stats) / T) if T else None
-            U = PF.resample_word(77, k)
-            uniform, Tt, offsets, ranges = PF.plan_resample(stats, P, n, U)
-            a, b = ranges[rank]
-            Quse = np.ones(n, np.int64) if uniform else Ql
-            C = np.cumsum(Quse)
-            cap = max(1, max(r1 - r0 for r0, r1 in ranges))
-            chunk = torch.zeros(4, cap, dtype=torch.float32)
-            for jj, j in enumerate(range(a, b)):
-                li = int(np.searchsorted(C, PF.position(j, Tt, P, U) - offsets[rank], side="right"))
-                chunk[:3, jj] = torch.from_numpy(local[:, li].copy())
-                chunk[3, jj] = torch.tensor([begin + li], dtype=torch.int32).view(torch.float32)
-            new = PF.exchange_chunks(chunk, ranges, begin, n, world)
-            local = np.ascontiguousarray(new[:3].numpy())
-            anc_local = new[3].contiguous().view(torch.int32).numpy()
-            # single-process oracle
-            ref_est = pf.estimate(Q, ref)
-            anc_ref = pf.resample(Q, pf.resample_U(77, k))
-            ref = np.ascontiguousarray(ref[:, anc_ref])
-            results.append((est, ref_est if T else None, np.array_equal(anc_local, anc_ref[begin:begin + n]),
-                            np.array_equal(local, ref[:, begin:begin + n])))
-        q.put((rank, results))
+    rng = np.random.default_rng(seed)
+    n = P // world
+    begin = rank * n
+    chunk = torch.zeros(PF.chunk_words(n), dtype=torch.int32)
+    Ql, local = PF.shard_views(chunk, n)
+    local[0], local[1], local[2] = 100.0, 90.0, 1.0
+    ref = np.empty((3, P), np.float32)
+    ref[0], ref[1], ref[2] = 100.0, 90.0, 1.0
+    allc = torch.zeros(world * PF.chunk_words(n), dtype=torch.int32)
+    view = PF.global_view(allc, world, n)
+    results = []
+    for k in range(1, frames + 1):
+        # identical global weights on every rank; each rank writes only its shard
+        Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
+        if k == 2:
+            Q[:] = 0                                  # T == 0 -> uniform fallback path
+        if k == 3:
+            Q[rng.random(P) < 0.9] = 0
+        lp = np.ascontiguousarray(local.numpy())
+        pf.predict(lp, begin, 77, k, (3.0, 3.0, 0.05), 224, 224, (0.5, 2.0))
+        local.copy_(torch.from_numpy(lp))
+        pf.predict(ref, 0, 77, k, (3.0, 3.0, 0.05), 224, 224, (0.5, 2.0))
+        Ql.copy_(torch.from_numpy(Q[begin:begin + n].copy()))
+        PF._all_gather_into(allc, chunk)
+        Qg, pg = _read_global(view, P)
+        layout_ok = np.array_equal(Qg, Q) and np.array_equal(pg.view(np.uint32), ref.view(np.uint32))
+        # device step, emulated: the fixed-order statistics and the global resample, this rank's slots
+        T, sums = pf.shard_stats(Qg, pg)
+        est = tuple(float(v) for v in sums / T) if T else None
+        anc = pf.resample(Qg, PF.resample_word(77, k))[begin:begin + n]
+        local.copy_(torch.from_numpy(np.ascontiguousarray(pg[:, anc])))
+        Ql.zero_()
+        # single-process oracle
+        ref_est = pf.estimate(Q, ref)
+        anc_ref = pf.resample(Q, pf.resample_U(77, k))
+        ref = np.ascontiguousarray(ref[:, anc_ref])
+        results.append((est, ref_est if T else None, layout_ok, np.array_equal(anc, anc_ref[begin:begin + n]),
+                        np.array_equal(local.numpy(), ref[:, begin:begin + n])))
+    q.put((rank, results))
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_two_rank_exchange_matches_oracle(world):
-    """world 2, and world 8 (the driver's 8-GPU layout at 4096 particles: 512 per rank; here 64 per rank)."""
+@pytest.mark.parametrize("world,P", [(2, 512), (2, 510), (8, 512)])
+def test_two_rank_exchange_matches_oracle(world, P):
+    """world 2 (also with an odd shard: 255 particles, a padded chunk), and world 8 (the driver's 8-GPU layout at
+    4096 particles: 512 per rank; here 64 per rank)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    P, frames = 512, 5
+    frames = 5
     procs = [ctx.Process(target=_worker, args=(r, world, port, P, 3, frames, q)) for r in range(world)]
     for p in procs:
         p.start()
@@ -101,11 +107,12 @@ def test_two_rank_exchange_matches_oracle(world):
         assert p.exitcode == 0
     for r in range(world):
         assert not isinstance(out[r], str), out[r]
-        for k, (est, ref_est, anc_ok, states_ok) in enumerate(out[r], start=1):
+        for k, (est, ref_est, layout_ok, anc_ok, states_ok) in enumerate(out[r], start=1):
+            assert layout_ok, f"rank {r} frame {k}: gathered chunks do not read back as the global arrays"
             assert anc_ok, f"rank {r} frame {k}: ancestors differ from the global oracle"
             assert states_ok, f"rank {r} frame {k}: states differ"
             if ref_est is not None:
-                np.testing.assert_allclose(est, ref_est, rtol=1e-12)
+                assert est == ref_est, f"rank {r} frame {k}: estimate bits differ from the oracle"
     # every rank computes the same estimate bits
     for k in range(frames):
         for r in range(1, world):

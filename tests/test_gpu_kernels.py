@@ -732,3 +732,65 @@ def test_resample_sharded_equals_global(G):
                        torch.from_numpy(p[:, r * n:(r + 1) * n].copy()).to(DEV), anc, st, cdf)
         got.append(anc.cpu().numpy())
     assert np.array_equal(np.concatenate(got), ref)
+
+
+@pytest.mark.parametrize("G", [1, 2, 8])
+@pytest.mark.parametrize("P,mode", [(7, "dense"), (4096, "dense"), (4096, "sparse"), (4096, "zero"),
+                                    (4096, "onehot"), (65536, "sparse")])
+def test_estimate_resample_global(G, P, mode):
+    """vpf_estimate_resample (the ParticleFilter product path) over G gathered shard chunks: every rank's slots get
+    the global oracle's ancestors and states bit for bit, the resample word drawn on the device equals SPEC S1's,
+    T is exact, and the fp64 sums are the same bits for every G (and as vpf_shard_stats over the whole set)."""
+    from vitparticlefiltertracker_amd.particle_filter import chunk_words, global_view, shard_views
+    if P % G:
+        pytest.skip("P not divisible by G")
+    rng = np.random.default_rng(P + G)
+    Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
+    if mode == "sparse":
+        Q[rng.random(P) < 0.9] = 0
+    if mode == "zero":
+        Q[:] = 0
+    if mode == "onehot":
+        Q[:] = 0
+        Q[P // 3] = 12345
+    p = rng.uniform(0, 224, (3, P)).astype(np.float32)
+    seed, frame = (1 << 40) + 17 * P, 9
+    ref = pf.resample(Q, pf.resample_U(seed, frame))
+    T_ref, sums_ref = pf.shard_stats(Q, p)
+    n = P // G
+    cw = chunk_words(n)
+    allc = torch.zeros(G * cw, dtype=torch.int32)
+    for r in range(G):
+        Qv, pv = shard_views(allc[r * cw:(r + 1) * cw], n)
+        Qv.copy_(torch.from_numpy(Q[r * n:(r + 1) * n].copy()))
+        pv.copy_(torch.from_numpy(p[:, r * n:(r + 1) * n].copy()))
+    allc = allc.to(DEV)
+    view = global_view(allc, G, n)
+    # the world-1 form ParticleFilter passes: its own Q and particle arrays, one shard of P
+    Qd, pd = torch.from_numpy(Q).to(DEV), torch.from_numpy(p).to(DEV)
+    view1 = (Qd, P, pd.view(-1), P, 3 * P, P)
+    cdf = torch.empty(P, device=DEV, dtype=torch.int64)
+    stats1 = torch.empty(4, device=DEV, dtype=torch.int64)
+    anc1 = torch.empty(P, device=DEV, dtype=torch.int32)
+    st1 = torch.empty(3, P, device=DEV)
+    vpf().estimate_resample(*view1, P, seed, frame, 0, P, anc1, st1, cdf, stats1)
+    assert np.array_equal(anc1.cpu().numpy(), ref)
+    assert np.array_equal(st1.cpu().numpy(), p[:, ref])
+    s1 = stats1.cpu()
+    assert int(s1[0]) == T_ref
+    if T_ref:
+        np.testing.assert_allclose(s1[1:].view(torch.float64).numpy(), sums_ref, rtol=1e-13)
+        To = torch.empty(1, device=DEV, dtype=torch.int64)
+        So = torch.empty(3, device=DEV, dtype=torch.float64)
+        vpf().shard_stats(Qd, pd, To, So)
+        assert torch.equal(s1[1:].view(torch.float64), So.cpu())
+    else:   # uniform fallback: the plain sums (estimate = sum / P)
+        np.testing.assert_allclose(s1[1:].view(torch.float64).numpy(), p.astype(np.float64).sum(axis=1), rtol=1e-13)
+    for r in range(G):
+        anc = torch.full((n,), -1, device=DEV, dtype=torch.int32)
+        st = torch.empty(3, n, device=DEV)
+        stats = torch.empty(4, device=DEV, dtype=torch.int64)
+        vpf().estimate_resample(*view, P, seed, frame, r * n, (r + 1) * n, anc, st, cdf, stats)
+        assert np.array_equal(anc.cpu().numpy(), ref[r * n:(r + 1) * n]), f"shard {r}: ancestors"
+        assert np.array_equal(st.cpu().numpy().view(np.uint32), p[:, ref[r * n:(r + 1) * n]].view(np.uint32))
+        assert torch.equal(stats.cpu(), s1), f"shard {r}: statistics bits depend on G"

@@ -62,6 +62,8 @@ SIGNATURES = {
     "vpf_cosine_weight_f32": [_P, _I64, _I32, _P, _F32, _I32, _P, _P, _P],
     "vpf_shard_stats": [_P, _P, _I64, _I64, _P, _P, _P],
     "vpf_resample": [_P, _I64, _I64, _I64, _I64, _I64, _U32, _I32, _I64, _I64, _P, _I64, _P, _P, _I64, _P, _P],
+    "vpf_estimate_resample": [_P, _I64, _P, _I64, _I64, _I64, _I64, _U64, _U32, _I64, _I64, _P, _P, _I64, _P, _P,
+                              _P],
 }
 
 

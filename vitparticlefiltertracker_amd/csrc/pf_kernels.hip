@@ -182,4 +182,146 @@ VPF_API int vpf_resample(const int64_t* Q, int64_t n_local, int64_t global_begin
     VPF_RETURN_LAUNCH();
 }
 
+// ---------------- estimate + resample over the global particle set (SPEC S6 + S7, device-resident) -------------
+// The product path (ParticleFilter): every rank holds the GLOBAL weights and states — its own arrays (world 1) or
+// the all-gathered shard chunks (world > 1, one fixed-size all-gather of 20 B per particle) — so the totals, the
+// CDF, the resample word and the ancestors of its own output slots are computed on the device with no host
+// round trip in between, and every rank (and every world size) sums in the same fixed order over the global
+// index: the estimate is bit-identical for any G. Global index i lives in shard r = i / n_shard at k = i % n_shard.
+struct GlobalView {
+    const int64_t* Q;
+    int64_t q_stride;      // int64 elements from shard r's Q to shard r + 1's
+    const float* p;        // shard 0's x row; y at + ld, s at + 2 ld
+    int64_t ld;
+    int64_t p_stride;      // floats from shard r's x row to shard r + 1's
+    uint32_t n_shard;
+    __device__ __forceinline__ int64_t off(uint32_t i, int64_t stride) const {
+        const uint32_t r = i / n_shard;
+        return (int64_t)r * stride + (int64_t)(i - r * n_shard);
+    }
+    __device__ __forceinline__ int64_t q(uint32_t i) const { return Q[off(i, q_stride)]; }
+    __device__ __forceinline__ const float* state(uint32_t i) const { return p + off(i, p_stride); }
+};
+
+// One workgroup: SPEC S6 sums in k_shard_stats' fixed tree (thread t takes i = t, t + 1024, ... in order, then
+// pairwise halving), repeated with every Q_i = 1 when T == 0 (the uniform fallback's plain sums); then the
+// inclusive int64 CDF (k_scan's chunked wave scan). stats_out = {T, bits of the three fp64 sums}.
+__global__ __launch_bounds__(1024) void k_stats_scan_global(GlobalView g, int64_t P, int64_t* __restrict__ cdf,
+                                                            int64_t* __restrict__ stats_out) {
+    __shared__ int64_t sT[1024];
+    __shared__ double sx[1024], sy[1024], sz[1024];
+    __shared__ int64_t wsum[16];
+    __shared__ int64_t carry_s;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    for (int pass = 0; pass < 2; ++pass) {
+        int64_t T = 0;
+        double ax = 0, ay = 0, az = 0;
+        for (int64_t i = t; i < P; i += 1024) {
+            const float* st = g.state((uint32_t)i);
+            const int64_t q = pass == 0 ? g.q((uint32_t)i) : (int64_t)1;
+            const double qd = (double)q;
+            T += q;
+            ax += qd * (double)st[0]; ay += qd * (double)st[g.ld]; az += qd * (double)st[2 * g.ld];
+        }
+        sT[t] = T; sx[t] = ax; sy[t] = ay; sz[t] = az;
+        __syncthreads();
+        for (int o = 512; o > 0; o >>= 1) {
+            if (t < o) {
+                sT[t] += sT[t + o]; sx[t] += sx[t + o]; sy[t] += sy[t + o]; sz[t] += sz[t + o];
+            }
+            __syncthreads();
+        }
+        const int64_t Tall = sT[0];
+        if (pass == 0 && t == 0) stats_out[0] = Tall;
+        if (pass == 1 || Tall != 0) {
+            if (t == 0) {
+                stats_out[1] = __double_as_longlong(sx[0]);
+                stats_out[2] = __double_as_longlong(sy[0]);
+                stats_out[3] = __double_as_longlong(sz[0]);
+            }
+            break;
+        }
+        __syncthreads();   // every thread has read sT[0] before pass 1 rewrites the tree
+    }
+    if (t == 0) carry_s = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < P; base += 4096) {
+        int64_t v[4];
+        int64_t loc = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t i = base + (int64_t)t * 4 + e;
+            loc += (i < P) ? g.q((uint32_t)i) : (int64_t)0;
+            v[e] = loc;
+        }
+        const int64_t incl = wave_incl_scan(loc, lane);
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        int64_t wprefix = 0;
+        for (int w = 0; w < wid; ++w) wprefix += wsum[w];
+        const int64_t excl = carry_s + wprefix + (incl - loc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t i = base + (int64_t)t * 4 + e;
+            if (i < P) cdf[i] = excl + v[e];
+        }
+        __syncthreads();
+        if (t == 1023) {
+            int64_t tot = 0;
+            for (int w = 0; w < 16; ++w) tot += wsum[w];
+            carry_s += tot;
+        }
+        __syncthreads();
+    }
+}
+
+// One thread per output slot j in [slot_begin, slot_end): T = cdf[P-1] (0 -> uniform: C_i = i + 1, so a_j =
+// pos_j), U = Philox(ctr = (0, frame, 1, 0), key = seed) word 0 (SPEC S1), pos_j exact (SPEC S7), a_j =
+// min{i : C_i > pos_j} by binary search over the global CDF, and the ancestor's state.
+__global__ __launch_bounds__(256) void k_resample_global(const int64_t* __restrict__ cdf, int64_t P, uint32_t k0,
+                                                         uint32_t k1, uint32_t frame, int64_t slot_begin,
+                                                         int64_t slot_end, GlobalView g, int32_t* __restrict__ anc,
+                                                         float* __restrict__ ox, float* __restrict__ oy,
+                                                         float* __restrict__ os) {
+    const int64_t jj = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t j = slot_begin + jj;
+    if (j >= slot_end) return;
+    const int64_t T = cdf[P - 1];
+    const uint32_t U = philox4x32_10(0u, frame, 1u, 0u, k0, k1).v[0];
+    const uint64_t pos = sys_position((uint64_t)j, (uint64_t)(T == 0 ? P : T), (uint64_t)P, U);
+    int64_t lo;
+    if (T == 0) {
+        lo = (int64_t)pos;
+    } else {
+        int64_t hi = P - 1;
+        lo = 0;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((uint64_t)cdf[mid] > pos) hi = mid; else lo = mid + 1;
+        }
+    }
+    const float* st = g.state((uint32_t)lo);
+    anc[jj] = (int32_t)lo;
+    ox[jj] = st[0]; oy[jj] = st[g.ld]; os[jj] = st[2 * g.ld];
+}
+
+VPF_API int vpf_estimate_resample(const int64_t* Q, int64_t q_stride, const float* particles, int64_t ld,
+                                  int64_t p_stride, int64_t n_shard, int64_t P, uint64_t seed, uint32_t frame,
+                                  int64_t slot_begin, int64_t slot_end, int32_t* anc_out, float* states_out,
+                                  int64_t out_ld, int64_t* cdf_ws, int64_t* stats_out, void* stream) {
+    if (P <= 0 || P > 0x7fffffffLL || n_shard <= 0 || P % n_shard != 0 || ld < n_shard || slot_begin < 0 ||
+        slot_end < slot_begin || slot_end > P || out_ld < slot_end - slot_begin)
+        return VPF_ERR_ARG;
+    if (P > n_shard && (q_stride < n_shard || p_stride < 2 * ld + n_shard)) return VPF_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const GlobalView g{Q, q_stride, particles, ld, p_stride, (uint32_t)n_shard};
+    hipLaunchKernelGGL(k_stats_scan_global, dim3(1), dim3(1024), 0, s, g, P, cdf_ws, stats_out);
+    const int64_t cnt = slot_end - slot_begin;
+    if (cnt > 0)
+        hipLaunchKernelGGL(k_resample_global, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, cdf_ws, P,
+                           (uint32_t)seed, (uint32_t)(seed >> 32), frame, slot_begin, slot_end, g, anc_out,
+                           states_out, states_out + out_ld, states_out + 2 * out_ld);
+    VPF_RETURN_LAUNCH();
+}
+
 VPF_API const char* vpf_version(void) { return "libvpf 0.1.0 gfx950"; }

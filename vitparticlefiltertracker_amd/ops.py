@@ -437,3 +437,28 @@ def resample(Q: torch.Tensor, global_begin: int, offset: int, total: int, P: int
     n_local = Q.numel()
     call("vpf_resample", ptr(Q), n_local, global_begin, offset, total, P, U, int(uniform), slot_begin, slot_end,
          ptr(particles), particles.shape[1], ptr(anc), ptr(states), states.shape[1], ptr(cdf_ws), stream_ptr())
+
+
+@torch.library.custom_op("vpf::estimate_resample", mutates_args={"anc", "states", "cdf_ws", "stats_out"},
+                         device_types="cuda")
+def estimate_resample(Q: torch.Tensor, q_stride: int, particles: torch.Tensor, ld: int, p_stride: int, n_shard: int,
+                      P: int, seed: int, frame: int, slot_begin: int, slot_end: int, anc: torch.Tensor,
+                      states: torch.Tensor, cdf_ws: torch.Tensor, stats_out: torch.Tensor) -> None:
+    """H11 + H12 over the global particle set (vpf_estimate_resample): Q int64 / particles f32 are flat views in the
+    shard layout (shard r's Q at r*q_stride, its x row at r*p_stride, y / s at + ld / + 2 ld); stats_out int64[4]."""
+    _dev(Q, particles, anc, states, cdf_ws, stats_out)
+    G = P // n_shard if n_shard > 0 else 0
+    _chk(Q.dtype == torch.int64 and particles.dtype == _F32, "estimate_resample: Q int64, particles f32")
+    _chk(G >= 1 and G * n_shard == P, "estimate_resample: P must be a multiple of n_shard")
+    _chk(Q.numel() >= (G - 1) * q_stride + n_shard, "estimate_resample: Q view too short for the shard layout")
+    _chk(particles.numel() >= (G - 1) * p_stride + 2 * ld + n_shard,
+         "estimate_resample: particle view too short for the shard layout")
+    cnt = slot_end - slot_begin
+    _chk(anc.dtype == torch.int32 and anc.numel() >= cnt, "estimate_resample: anc int32[>= slots]")
+    _chk(states.dtype == _F32 and states.dim() == 2 and states.shape[0] == 3 and states.shape[1] >= cnt,
+         "estimate_resample: states f32[3][>= slots]")
+    _chk(cdf_ws.dtype == torch.int64 and cdf_ws.numel() >= P, "estimate_resample: cdf_ws int64[P]")
+    _chk(stats_out.dtype == torch.int64 and stats_out.numel() >= 4, "estimate_resample: stats_out int64[4]")
+    call("vpf_estimate_resample", ptr(Q), q_stride, ptr(particles), ld, p_stride, n_shard, P, seed & (2**64 - 1),
+         frame & 0xFFFFFFFF, slot_begin, slot_end, ptr(anc), ptr(states), states.shape[1], ptr(cdf_ws),
+         ptr(stats_out), stream_ptr())

@@ -2,17 +2,18 @@
 estimation" (/root/reference/README.md:8), SPEC.md S2/S5-S7, on the HIP path.
 
 Particles are sharded by index across ranks (rank r owns [r*P/G, (r+1)*P/G)); one process per GPU.
-Per frame the only cross-device traffic is:
+Per frame the only cross-device traffic is ONE fixed-size all-gather of the shard chunks (weight Q_i int64 +
+state x, y, s fp32 = 20 B per particle; 80 KB at 4096 particles, 1.3 MB at configs[4]'s 65536). Every rank then
+holds the global weights and states, and one device call (vpf_estimate_resample) computes on each rank:
 
-  1. an all-gather of each shard's 32-byte statistics {T_r (int64), sum Q*x, sum Q*y, sum Q*s (fp64)}.
-     It provides the global weight normaliser T (the "weight-normalisation sum"), the shard offsets
-     O_r = sum_{q<r} T_q that make the integer systematic resample exact and shard-invariant, and the
-     estimate, summed in rank order so every rank computes the same bits;
-  2. an all-gather of the resampled chunks (ancestor index + state, 16 B per slot, padded to the largest
-     chunk) from which each rank keeps the slots it owns for the next frame.
+  * the weight-normalisation sum T and the estimate sums (SPEC S6), in one fixed-order tree over the GLOBAL
+    index, so every rank and every world size gets the same bits;
+  * the inclusive CDF and, from the resample word drawn on the device, the exact systematic-resample ancestors
+    of the slots this rank owns (SPEC S7): identical to the single-process oracle for any G.
 
-Both run on torch.distributed (backend "nccl" = RCCL over xGMI on the GPU box; "gloo" in CPU tests of the
-exchange logic). With G = 1 there is no collective.
+No host planning sits between the weights and the resample; the host reads only the 32-B statistics (the
+estimate it returns). The collective runs on torch.distributed (backend "nccl" = RCCL over xGMI on the GPU box;
+"gloo" in CPU tests of the layout and when several ranks share one GPU). With G = 1 there is no collective.
 """
 from __future__ import annotations
 
@@ -67,6 +68,21 @@ def slot_range(offset: int, shard_T: int, T: int, P: int, U: int) -> Tuple[int, 
     return first_at_least(offset), first_at_least(offset + shard_T)
 
 
+def plan_resample(stats, P: int, n_local: int, U: int):
+    """Host plan of the exact systematic resample (SPEC S7) for the per-shard entry point vpf_resample, from the
+    shards' (T_r, ...) statistics: (uniform, T, offsets, slot ranges per rank). ParticleFilter itself runs the
+    device-resident vpf_estimate_resample and needs no plan."""
+    world = len(stats)
+    T_r = [s[0] for s in stats]
+    uniform = sum(T_r) == 0
+    if uniform:
+        T_r = [n_local] * world
+    T = sum(T_r)
+    offsets = [sum(T_r[:r]) for r in range(world)]
+    ranges = [slot_range(offsets[r], T_r[r], T, P, U) for r in range(world)]
+    return uniform, T, offsets, ranges
+
+
 def _all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
     """all_gather_into_tensor on the group's backend. RCCL ("nccl") takes the device tensors directly, on the
     current stream. gloo (CPU tests; several ranks sharing one GPU) exchanges host copies."""
@@ -79,53 +95,33 @@ def _all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
         dist.all_gather_into_tensor(out, inp, group=group)
 
 
-def gather_stats(packed: torch.Tensor, world_size: int, group=None) -> List[Tuple[int, float, float, float]]:
-    """All-gather each shard's packed int64[4] = {T_r, bits of sum Qx, sum Qy, sum Qs} and decode on the host.
-    Works for any device / backend (RCCL on the GPU box, gloo on CPU)."""
-    if world_size > 1:
-        allp = torch.empty(world_size * 4, dtype=torch.int64, device=packed.device)
-        _all_gather_into(allp, packed.contiguous().view(-1), group)
-        allp = allp.view(world_size, 4)
-    else:
-        allp = packed.view(1, 4)
-    host = allp.cpu()
-    T_r = host[:, 0].tolist()
-    sums = host[:, 1:].contiguous().view(torch.float64).tolist()
-    return [(int(T_r[r]), *sums[r]) for r in range(world_size)]
+def chunk_words(n: int) -> int:
+    """int32 words of one shard chunk: Q int64[n] | x | y | s fp32[n], padded to a multiple of 8 bytes."""
+    return 5 * n + (n & 1)
 
 
-def plan_resample(stats, P: int, n_local: int, U: int):
-    """Host plan of the exact systematic resample (SPEC S7) from the gathered shard statistics:
-    (uniform, T, offsets, slot ranges per rank)."""
-    world = len(stats)
-    T_r = [s[0] for s in stats]
-    uniform = sum(T_r) == 0
-    if uniform:
-        T_r = [n_local] * world
-    T = sum(T_r)
-    offsets = [sum(T_r[:r]) for r in range(world)]
-    ranges = [slot_range(offsets[r], T_r[r], T, P, U) for r in range(world)]
-    return uniform, T, offsets, ranges
+def shard_views(chunk: torch.Tensor, n: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(Q int64[n], particles f32[3][n]) as views into one shard chunk (int32[chunk_words(n)]): the filter's
+    state lives in the chunk, so the all-gather sends it as is (no packing)."""
+    return chunk[: 2 * n].view(torch.int64), chunk[2 * n: 5 * n].view(torch.float32).view(3, n)
 
 
-def exchange_chunks(chunk: torch.Tensor, ranges, begin: int, n_local: int, world_size: int, group=None):
-    """All-gather the padded per-rank resample chunks ([4][cap] = x, y, s, ancestor bits) and keep the slots
-    [begin, begin + n_local) this rank owns. Returns [4][n_local]."""
-    cap = chunk.shape[1]
-    allc = torch.empty(world_size * 4 * cap, device=chunk.device, dtype=chunk.dtype)
-    _all_gather_into(allc, chunk.contiguous().view(-1), group)
-    allc = allc.view(world_size, 4, cap)
-    parts = []
-    for r, (ra, rb) in enumerate(ranges):
-        lo, hi = max(ra, begin), min(rb, begin + n_local)
-        if lo < hi:
-            parts.append(allc[r, :, lo - ra: hi - ra])
-    return torch.cat(parts, dim=1)
+def global_view(allc: torch.Tensor, world: int, n: int):
+    """Kernel arguments of vpf_estimate_resample for `world` gathered chunks of n particles each (allc:
+    int32[world * chunk_words(n)]): (Q view, q_stride, particle view, ld, p_stride, n_shard)."""
+    cw = chunk_words(n)
+    return allc.view(torch.int64), cw // 2, allc[2 * n:].view(torch.float32), n, cw, n
 
 
 class ParticleFilter:
     """H1, H10-H12. API: predict(), update(features, template), estimate(), resample(),
-    attributes `particles` (float32[3][P_local] on the device, SoA rows x, y, scale) and `Q` (int64[P_local])."""
+    attributes `particles` (float32[3][P_local] on the device, SoA rows x, y, scale) and `Q` (int64[P_local]).
+
+    Both attributes are views into one shard chunk (`shard_views`). Per frame (`step`, or estimate() then
+    resample()): world > 1 all-gathers the chunks (20 B per particle, one fixed-size RCCL collective), then ONE
+    device call, vpf_estimate_resample, computes the estimate sums, the CDF, the resample word and the ancestors
+    of this rank's slots over the global set. The resample is enqueued before the host waits for the 32-B
+    statistics, so the only host synchronisation of a frame is that read."""
 
     def __init__(self, num_particles: int, init_state=(0.0, 0.0, 1.0), motion_std=(4.0, 4.0, 0.02),
                  scale_range=(0.5, 2.0), seed: int = 1234, device=None, frame_size=(224, 224),
@@ -139,7 +135,7 @@ class ParticleFilter:
             raise ValueError("lam must be finite and >= 0 (SPEC S5)")
         self.P = int(num_particles)
         self.rank, self.world_size, self.group = int(rank), int(world_size), group
-        self.n_local = self.P // self.world_size
+        self.n_local = n = self.P // self.world_size
         self.begin = self.rank * self.n_local
         self.motion_std = [float(v) for v in motion_std]
         self.scale_range = [float(v) for v in scale_range]
@@ -147,16 +143,23 @@ class ParticleFilter:
         self.lam, self.bits = float(lam), int(weight_bits)
         self.height, self.width = int(frame_size[0]), int(frame_size[1])
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.particles = torch.empty(3, self.n_local, device=self.device, dtype=torch.float32)
-        self.Q = torch.zeros(self.n_local, device=self.device, dtype=torch.int64)
-        self._T = torch.zeros(1, device=self.device, dtype=torch.int64)
-        self._sums = torch.zeros(3, device=self.device, dtype=torch.float64)
-        self._cdf = torch.empty(self.n_local, device=self.device, dtype=torch.int64)
-        self._states = torch.empty(3, self.n_local, device=self.device, dtype=torch.float32)
-        self._anc = torch.empty(self.n_local, device=self.device, dtype=torch.int32)
+        self._chunk = torch.zeros(chunk_words(n), device=self.device, dtype=torch.int32)
+        self.Q, self.particles = shard_views(self._chunk, n)
+        if self.world_size > 1:
+            self._allc = torch.zeros(self.world_size * chunk_words(n), device=self.device, dtype=torch.int32)
+            self._gview = global_view(self._allc, self.world_size, n)
+        else:
+            self._gview = (self.Q, n, self.particles.view(-1), n, 3 * n, n)
+        self._cdf = torch.empty(self.P, device=self.device, dtype=torch.int64)
+        self._states = torch.empty(3, n, device=self.device, dtype=torch.float32)
+        self._anc = torch.empty(n, device=self.device, dtype=torch.int32)
+        self._stats_dev = torch.zeros(4, device=self.device, dtype=torch.int64)
+        self._stats_pin = torch.zeros(4, dtype=torch.int64).pin_memory()
+        self._stats_evt = torch.cuda.Event()
         self.frame = 0
         self.last_ancestors: Optional[torch.Tensor] = None
-        self._stats_host: Optional[List[Tuple[int, float, float, float]]] = None
+        self._settled = False                                   # estimate / resample of the current Q computed
+        self._est: Optional[Tuple[float, float, float]] = None  # its host value once read
         self.reset(init_state)
 
     # ------------------------------------------------------------------ state
@@ -167,14 +170,14 @@ class ParticleFilter:
         self.particles[2].fill_(s)
         self.Q.zero_()
         self.frame = 0
-        self._stats_host = None
+        self._settled = False
 
     def predict(self, frame: Optional[int] = None) -> None:
         """H1: counter-based random walk (SPEC S2) for frame index `frame` (default: next frame)."""
         self.frame = self.frame + 1 if frame is None else int(frame)
         vpf.predict_(self.particles, self.begin, self.seed, self.frame, self.motion_std, float(self.width),
                      float(self.height), self.scale_range)
-        self._stats_host = None
+        self._settled = False
 
     def update(self, features: torch.Tensor, template: torch.Tensor) -> torch.Tensor:
         """H10 from explicit features [n][D] fp32 (LN'd CLS) and a unit template [D]: sets Q."""
@@ -183,65 +186,62 @@ class ParticleFilter:
             raise ValueError(f"update: expected {self.n_local} feature rows, got {n}")
         vpf.cosine_weight(features.to(torch.float32).contiguous(), template.to(torch.float32).contiguous(),
                           self.lam, self.bits, self.Q, None)
-        self._stats_host = None
+        self._settled = False
         return self.Q
 
     def set_weights(self, Q: torch.Tensor) -> None:
         if Q.data_ptr() != self.Q.data_ptr():
             self.Q.copy_(Q)
-        self._stats_host = None
+        self._settled = False
 
-    # ------------------------------------------------------------------ H11
-    def _gather_stats(self) -> List[Tuple[int, float, float, float]]:
-        if self._stats_host is None:
-            vpf.shard_stats(self.Q, self.particles, self._T, self._sums)
-            packed = torch.cat([self._T, self._sums.view(torch.int64)])          # 4 x int64 = 32 B
-            self._stats_host = gather_stats(packed, self.world_size, self.group)
-        return self._stats_host
+    # ------------------------------------------------------------------ H11 + H12 on the device
+    def _settle(self) -> None:
+        """Enqueue (world > 1: the chunk all-gather, then) vpf_estimate_resample for the current weights and the
+        32-B statistics' copy to pinned host memory. No host synchronisation."""
+        if self._settled:
+            return
+        if self.world_size > 1:
+            _all_gather_into(self._allc, self._chunk, self.group)
+        Qv, qs, Pv, ld, ps, nsh = self._gview
+        vpf.estimate_resample(Qv, qs, Pv, ld, ps, nsh, self.P, self.seed, self.frame, self.begin,
+                              self.begin + self.n_local, self._anc, self._states, self._cdf, self._stats_dev)
+        self._stats_pin.copy_(self._stats_dev, non_blocking=True)
+        self._stats_evt.record()
+        self._settled = True
+        self._est = None
+
+    def _commit(self) -> None:
+        """Enqueue the resample computed by _settle: this rank's slots take their ancestors' states."""
+        self.particles.copy_(self._states)
+        self.last_ancestors = self._anc.clone()
+        self.Q.zero_()
+        self._settled = False
+
+    def _read_estimate(self) -> Tuple[float, float, float]:
+        """SPEC S6 from the settled statistics (waits for their D2H copy): sum Q*state / T, or the plain mean
+        when T == 0. The sums are the same bits on every rank and for every world size."""
+        if self._est is None:
+            self._stats_evt.synchronize()
+            T = int(self._stats_pin[0])
+            sx, sy, ss = self._stats_pin[1:].view(torch.float64).tolist()
+            d = float(T) if T else float(self.P)
+            self._est = (sx / d, sy / d, ss / d)
+        return self._est
 
     def estimate(self) -> Tuple[float, float, float]:
-        """SPEC S6: weighted mean state; every rank returns the same bits (rank-order sums)."""
-        st = self._gather_stats()
-        T = sum(s[0] for s in st)
-        if T == 0:
-            m = self.particles.to(torch.float64).sum(dim=1)
-            if self.world_size > 1:
-                allm = torch.empty(self.world_size * 3, dtype=torch.float64, device=m.device)
-                _all_gather_into(allm, m.contiguous(), self.group)
-                m = allm.view(self.world_size, 3).sum(dim=0)
-            m = (m / self.P).tolist()
-            return float(m[0]), float(m[1]), float(m[2])
-        sx = sy = ss = 0.0
-        for s in st:
-            sx += s[1]; sy += s[2]; ss += s[3]
-        return sx / T, sy / T, ss / T
+        """SPEC S6: weighted mean state of the current particles and weights."""
+        self._settle()
+        return self._read_estimate()
 
-    # ------------------------------------------------------------------ H12
     def resample(self) -> torch.Tensor:
         """SPEC S7 systematic resample; returns the global ancestor indices of this rank's slots."""
-        st = self._gather_stats()
-        U = resample_word(self.seed, self.frame)
-        uniform, T, offsets, ranges = plan_resample(st, self.P, self.n_local, U)
-        a, b = ranges[self.rank]
-        cnt = b - a
-        if self.world_size == 1:
-            vpf.resample(self.Q, self.begin, offsets[0], T, self.P, U, uniform, 0, self.P, self.particles, self._anc,
-                         self._states, self._cdf)
-            self.particles.copy_(self._states)
-            self.last_ancestors = self._anc.clone()
-        else:
-            cap = max(1, max(r[1] - r[0] for r in ranges))
-            chunk = torch.zeros(4, cap, device=self.device, dtype=torch.float32)
-            if cnt > 0:
-                anc_c = torch.empty(cnt, device=self.device, dtype=torch.int32)
-                states_c = torch.empty(3, cnt, device=self.device, dtype=torch.float32)
-                vpf.resample(self.Q, self.begin, offsets[self.rank], T, self.P, U, uniform, a, b, self.particles,
-                             anc_c, states_c, self._cdf)
-                chunk[:3, :cnt] = states_c
-                chunk[3, :cnt] = anc_c.view(torch.float32)
-            new = exchange_chunks(chunk, ranges, self.begin, self.n_local, self.world_size, self.group)
-            self.particles.copy_(new[:3])
-            self.last_ancestors = new[3].contiguous().view(torch.int32)
-        self.Q.zero_()
-        self._stats_host = None
+        self._settle()
+        self._commit()
         return self.last_ancestors
+
+    def step(self) -> Tuple[float, float, float]:
+        """estimate() then resample() of one frame, with the resample enqueued before the host waits for the
+        estimate (Tracker.track)."""
+        self._settle()
+        self._commit()
+        return self._read_estimate()

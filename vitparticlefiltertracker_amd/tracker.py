@@ -8,8 +8,8 @@ positions", README.md:42). SPEC.md S8 / SURVEY.md §8a H13-H14.
     for f in frames: x, y, s = t.track(f)
 
 Per frame: predict (eager launch; its frame index is a kernel argument) -> [HIP graph replay: crop+ViT
--> final LN -> cosine -> Q] -> shard stats (+ 32-B all-gather across ranks) -> estimate -> resample
-(+ chunk all-gather across ranks). The only host synchronisation is reading the shard statistics.
+-> final LN -> cosine -> Q] -> (world > 1: one all-gather of the shard chunks) -> estimate + resample on the
+device (vpf_estimate_resample). The only host synchronisation is reading the 32-B estimate statistics.
 """
 from __future__ import annotations
 
@@ -169,10 +169,11 @@ class Tracker:
         self.frame_index += 1
         self.pf.predict(self.frame_index)
         self.weigh()
-        est = self.pf.estimate()
+        # estimate + resample on the device, the resample enqueued before the host reads the estimate; the template
+        # update crops at the estimate on this frame and does not read the particles
+        est = self.pf.step()
         if self.template_alpha > 0.0:
             self.update_template(est)
-        self.pf.resample()
         return est
 
     def update_template(self, state, alpha: Optional[float] = None) -> None:
@@ -289,9 +290,8 @@ class MultiTracker:
             self._graph.replay()
         else:
             self._forward()
-        out = []
-        for k, pf in enumerate(self.pfs):
+        for k, pf in enumerate(self.pfs):       # every target's estimate + resample enqueued, then one wait
             pf.set_weights(self.engine.Q[k * self.P:(k + 1) * self.P])
-            out.append(pf.estimate())
-            pf.resample()
-        return out
+            pf._settle()
+            pf._commit()
+        return [pf._read_estimate() for pf in self.pfs]
