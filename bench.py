@@ -36,21 +36,24 @@ PEAK_BF16_TFLOPS = 2500.0     # dense bf16 MFMA, /opt/skills/guides/MI355X_MICRO
 PEAK_FP8_TFLOPS = 5000.0      # dense block-scaled e4m3 MFMA (same table), the fp8 path's GEMMs
 
 
-# newest committed PMC summary first (profiles/r<round>_pmc_traffic.json)
-PMC_TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f"r{r}_pmc_traffic.json") for r in (2, 1)]
+# newest committed PMC summary first (profiles/r<round>_pmc_traffic[_<dtype>].json)
+def _pmc_files(dtype: str):
+    suffix = "" if dtype == "bf16" else f"_{dtype}"
+    return [os.path.join(ROOT, "profiles", f"r{r}_pmc_traffic{suffix}.json") for r in (2, 1)]
 
 
-def pmc_traffic(arch_name: str, n_local: int, kernel: str):
+def pmc_traffic(arch_name: str, n_local: int, kernel: str, dtype: str = "bf16"):
     """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_traffic.py over two
     rocprofv3 passes of this bench: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when it was taken on the
     same workload; otherwise (None, reason)."""
-    for path in PMC_TRAFFIC_FILES:
+    for path in _pmc_files(dtype):
         if not os.path.exists(path):
             continue
         try:
             with open(path) as f:
                 d = json.load(f)
-            if d.get("arch") != arch_name or int(d.get("particles_per_gpu", -1)) != n_local:
+            if (d.get("arch") != arch_name or int(d.get("particles_per_gpu", -1)) != n_local
+                    or d.get("dtype", "bf16") != dtype):
                 return None, "no PMC summary for this workload"
             k = d["kernels"][kernel]
             return int(k["traffic_bytes"]), os.path.relpath(path, ROOT)
@@ -221,7 +224,8 @@ def main() -> int:
             v["tflops"] = flops[name] / (v["avg_ms"] * 1e-3) / 1e12
     dom = max((n for n in flops if n.startswith("gemm") and n in ks), key=lambda n: ks[n]["total_ms"])
     ach = ks[dom]["tflops"]
-    traffic, traffic_src = pmc_traffic(args.arch, n_loc, dom) if args.dtype == "bf16" else (None, None)
+    traffic, traffic_src = (pmc_traffic(args.arch, n_loc, dom, args.dtype) if args.dtype in ("bf16", "fp8")
+                            else (None, None))
     # the dominant GEMM's MFMA peak: dense bf16, or dense MX-fp8 for the fp8 path's block-scaled GEMMs
     peak = PEAK_FP8_TFLOPS if args.dtype == "fp8" and dom in ("gemm_qkv", "gemm_fc1", "gemm_fc2") else PEAK_BF16_TFLOPS
     gflop_frame = arch.gflop_per_crop() * args.particles

@@ -20,6 +20,11 @@ def main(argv=None) -> int:
     ap.add_argument("--out", default=None, help="write positions as JSON here")
     ap.add_argument("--video-out", default=None,
                     help="write the frames with the tracked box drawn: a .y4m file, or a directory of .ppm frames")
+    ap.add_argument("--checkpoint", default=None,
+                    help="save the tracker state (np.savez; per rank with several GPUs) here after the last frame")
+    ap.add_argument("--checkpoint-every", type=int, default=0, help="also save every N frames")
+    ap.add_argument("--resume", default=None,
+                    help="continue from a checkpoint: the source's frames up to its frame index are skipped")
     args = ap.parse_args(argv)
 
     import torch
@@ -41,7 +46,14 @@ def main(argv=None) -> int:
     frames = prefetch(src, depth=2)   # decode + pin on a host thread, overlapped with the GPU frame loop
     tr = Tracker(cfg)
     first = next(frames)
-    tr.init(first, inp["bbox0"])
+    start = 1
+    if args.resume:
+        tr.load_checkpoint(args.resume)
+        for _ in range(tr.frame_index):       # frames 1 .. frame_index were tracked before the checkpoint
+            next(frames)
+        start = tr.frame_index + 1
+    else:
+        tr.init(first, inp["bbox0"])
     sink = None
     if args.video_out and tr.rank == 0:
         if args.video_out.lower().endswith(".y4m"):
@@ -58,15 +70,20 @@ def main(argv=None) -> int:
         else:
             write_ppm(os.path.join(args.video_out, f"frame_{k:05d}.ppm"), img)
 
-    emit(0, first, inp["bbox0"])
+    if not args.resume:
+        emit(0, first, inp["bbox0"])
     t0 = time.perf_counter()
     out = []
-    for k, f in enumerate(frames, start=1):
+    for k, f in enumerate(frames, start=start):
         x, y, s = tr.track(f)
         out.append({"frame": k, "x": x, "y": y, "scale": s})
         emit(k, f, tr.box((x, y, s)))
         if tr.rank == 0:
             print(f"frame {k:4d}  x={x:8.2f}  y={y:8.2f}  scale={s:6.3f}", flush=True)
+        if args.checkpoint and args.checkpoint_every > 0 and k % args.checkpoint_every == 0:
+            tr.save_checkpoint(args.checkpoint)
+    if args.checkpoint:
+        tr.save_checkpoint(args.checkpoint)
     if sink is not None:
         sink.close()
     dt = time.perf_counter() - t0

@@ -305,3 +305,66 @@ def test_tracker_upload_mixed_sources_and_size_change():
     assert (tr.pf.height, tr.pf.width) == (100, 120)
     p = tr.pf.particles.cpu().numpy()
     assert p[0].max() <= 119 and p[1].max() <= 99 and p.min() >= 0
+
+
+@pytest.mark.parametrize("alpha", [0.0, 0.5])
+def test_checkpoint_resume_bit_exact(tmp_path, alpha):
+    """SURVEY.md §5 checkpoint / resume: 3 frames, save_checkpoint, a NEW Tracker loads it and tracks frames 4-6:
+    estimates, ancestors and particle states equal an uninterrupted run bit for bit (counter-based noise; with a
+    template update the updated template travels in the checkpoint). A second uninterrupted run is also
+    bit-identical to the first (the run-to-run determinism check that stands in for a race detector)."""
+    from vitparticlefiltertracker_amd import Tracker
+    cfg = load_config({"model": {"arch": "vit_tiny_patch16_224", "dtype": "bf16", "weights": {"seed": 3}},
+                       "particles": {"num": 256, "seed": 99}, "likelihood": {"template_update": alpha}})
+    w = make_vit_weights(ARCHS["vit_tiny_patch16_224"], seed=3)
+    clip = synthetic_clip(7)
+
+    def run(tr, frames):
+        return [(tr.track(f), tr.pf.last_ancestors.cpu().numpy().copy(), tr.pf.particles.cpu().numpy().copy())
+                for f in frames]
+
+    tr = Tracker(cfg, weights=w)
+    tr.init(clip[0], (80, 80, 64, 64))
+    ref = run(tr, clip[1:])
+    tr = Tracker(cfg, weights=w)
+    tr.init(clip[0], (80, 80, 64, 64))
+    again = run(tr, clip[1:])
+    a = Tracker(cfg, weights=w)
+    a.init(clip[0], (80, 80, 64, 64))
+    first = run(a, clip[1:4])
+    path = a.save_checkpoint(str(tmp_path / "ck"))
+    del a
+    b = Tracker(cfg, weights=w)
+    b.load_checkpoint(path)
+    assert b.frame_index == 3
+    rest = run(b, clip[4:])
+    for k, (r, g, h) in enumerate(zip(ref, first + rest, again), start=1):
+        assert r[0] == g[0] == h[0], f"frame {k}: estimate"
+        assert np.array_equal(r[1], g[1]) and np.array_equal(r[1], h[1]), f"frame {k}: ancestors"
+        assert np.array_equal(r[2].view(np.uint32), g[2].view(np.uint32)), f"frame {k}: particles"
+        assert np.array_equal(r[2].view(np.uint32), h[2].view(np.uint32)), f"frame {k}: particles (rerun)"
+    with pytest.raises(ValueError, match="configuration"):
+        other = Tracker(load_config({"model": {"arch": "vit_tiny_patch16_224", "dtype": "bf16"},
+                                     "particles": {"num": 128, "seed": 99}}), weights=w)
+        other.load_checkpoint(path)
+
+
+def test_main_checkpoint_resume(tmp_path):
+    """main.py --checkpoint after 3 frames, then --resume for the rest: the positions equal one uninterrupted run."""
+    import json
+    import sys
+    import yaml
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+    import main as vpf_main
+    cfg = {"model": {"arch": "vit_tiny_patch16_224", "dtype": "bf16"}, "particles": {"num": 128, "seed": 5},
+           "input": {"source": "synthetic", "frames": 7}}
+    cpath = tmp_path / "config.yaml"
+    cpath.write_text(yaml.safe_dump(cfg))
+    full, part1, part2 = tmp_path / "full.json", tmp_path / "p1.json", tmp_path / "p2.json"
+    ck = str(tmp_path / "state")
+    assert vpf_main.main(["--config", str(cpath), "--out", str(full)]) == 0
+    assert vpf_main.main(["--config", str(cpath), "--frames", "4", "--out", str(part1), "--checkpoint", ck]) == 0
+    assert vpf_main.main(["--config", str(cpath), "--out", str(part2), "--resume", ck]) == 0
+    a, b, c = (json.loads(p.read_text()) for p in (full, part1, part2))
+    assert [r["frame"] for r in b] == [1, 2, 3] and [r["frame"] for r in c] == [4, 5, 6]
+    assert a == b + c

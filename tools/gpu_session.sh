@@ -41,6 +41,17 @@ for step in "$@"; do
       ok_or_stop $? pmc_write
       python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write > $OUT/pmc_traffic.json 2> $OUT/pmc_traffic.err
       ok_or_stop $? pmc_traffic; cat $OUT/pmc_traffic.json | head -40 ;;
+    pmc8)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc8_fetch -o p --output-format csv -- python3 bench.py --dtype fp8 --steps 1 --warmup 1 --kernel-frames 1 --cpu-seconds 0 --no-graph > $OUT/pmc8_fetch.log 2>&1
+      ok_or_stop $? pmc8_fetch
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc8_write -o p --output-format csv -- python3 bench.py --dtype fp8 --steps 1 --warmup 1 --kernel-frames 1 --cpu-seconds 0 --no-graph > $OUT/pmc8_write.log 2>&1
+      ok_or_stop $? pmc8_write
+      python tools/pmc_traffic.py $OUT/pmc8_fetch $OUT/pmc8_write --dtype fp8 > $OUT/pmc_traffic_fp8.json 2> $OUT/pmc8_traffic.err
+      ok_or_stop $? pmc8_traffic; head -40 $OUT/pmc_traffic_fp8.json ;;
+    bench8)
+      timeout -k 10 900 python bench.py --dtype fp8 --steps 5 --warmup 2 --cpu-seconds 0 > $OUT/bench8.log 2>&1
+      ok_or_stop $? bench8; tail -1 $OUT/bench8.log | cut -c1-600 ;;
     lab)
       timeout -k 10 600 tools/gemm_lab/gemm_lab 5 "$LAB_SHAPES" "$LAB_VARS" 1 > $OUT/lab.log 2>&1
       ok_or_stop $? lab; grep -v "inf TFLOP" $OUT/lab.log | tail -40 ;;

@@ -5,11 +5,12 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the byte
 streaming read, so fetch bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE (KiB) is exact for 16-B-per-lane stores.
 Both count memory-side requests of the L2, Infinity-Cache hits included, i.e. an upper bound on HBM bytes.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> [--arch vit_base_patch16_224 --particles 4096]
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> [--arch vit_base_patch16_224 --particles 4096 --dtype bf16]
 
-Kernel naming: k_gemm_bf16<4> = QKV (LN epilogue), <5> = FC1 (LN + GELU), <3> = patch embed, and the two
-full-size <2> (bias + residual) launches of each block alternate proj, FC2 (dispatch order). CLS-row launches
-(grid of one M tile) are skipped.
+Kernel naming: k_gemm_bf16<4> / k_gemm_mx8<4> = QKV (LN epilogue), <5> = FC1 (LN + GELU), <3> = patch embed, and
+the two full-size <2> (bias + residual) launches of each block alternate proj, FC2 (dispatch order). CLS-row
+launches (grid of one M tile) are skipped. --dtype fp8: the MX8 GEMMs' algorithmic bytes count e4m3 elements
+(1 B) plus one e8m0 scale byte per 32 (configs[4]'s path: QKV / FC1 / FC2 / proj on MX8 operands).
 """
 import argparse
 import csv
@@ -37,9 +38,10 @@ def load(d, counter):
 def name_gemms(rows, min_grid):
     out, res_toggle = [], 0
     for _, kname, grid, val in rows:
-        if "k_gemm_bf16<" not in kname or grid < min_grid:
+        tag = "k_gemm_bf16<" if "k_gemm_bf16<" in kname else "k_gemm_mx8<" if "k_gemm_mx8<" in kname else None
+        if tag is None or grid < min_grid:
             continue
-        epi = kname.split("k_gemm_bf16<")[1].split(">")[0].split(",")[0].strip()
+        epi = kname.split(tag)[1].split(">")[0].split(",")[0].strip()
         if epi == "4":
             n = "gemm_qkv"
         elif epi == "5":
@@ -61,6 +63,7 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--arch", default="vit_base_patch16_224")
     ap.add_argument("--particles", type=int, default=4096)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     a = ap.parse_args()
     from vitparticlefiltertracker_amd.config import ARCHS
     arch = ARCHS[a.arch]
@@ -75,7 +78,17 @@ def main():
     alg = {"gemm_qkv": (M * D + 3 * D * D + M * 3 * D) * 2, "gemm_proj": (M * D + D * D + 2 * M * D) * 2,
            "gemm_fc1": (M * D + F * D + M * F) * 2, "gemm_fc2": (M * F + F * D + 2 * M * D) * 2,
            "gemm_patch": (a.particles * arch.n_patches * (arch.patch_kp + D) + D * arch.patch_kp) * 2}
-    res = {"arch": a.arch, "particles_per_gpu": a.particles,
+    if a.dtype == "fp8":
+        q = 33 / 32                                   # e4m3 element + its share of the e8m0 scale
+        # QKV: MX8 A, MX8 W, bf16 out; proj: MX8 A + W, bf16 residual in / out + the MX8 copy of h; FC1: MX8 in / W,
+        # MX8 hidden out only; FC2: MX8 hidden + W, bf16 residual in / out + the MX8 copy of h
+        alg.update({"gemm_qkv": (M * D + 3 * D * D) * q + M * 3 * D * 2,
+                    "gemm_proj": (M * D + D * D) * q + 2 * M * D * 2 + M * D * q,
+                    "gemm_fc1": (M * D + F * D + M * F) * q,
+                    "gemm_fc2": (M * F + F * D) * q + 2 * M * D * 2 + M * D * q,
+                    "gemm_patch": alg["gemm_patch"] + M * D * q})
+        alg = {k: int(v) for k, v in alg.items()}
+    res = {"arch": a.arch, "particles_per_gpu": a.particles, "dtype": a.dtype,
            "note": "fetch = 2 x FETCH_SIZE (gfx950 wide-read correction), write = WRITE_SIZE; KiB -> bytes; "
                    "memory-side L2 requests (Infinity-Cache hits included)", "kernels": {}}
     for n, v in sorted(acc.items()):

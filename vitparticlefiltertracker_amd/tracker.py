@@ -186,6 +186,65 @@ class Tracker:
         t = (1.0 - a) * self.template + a * (f / f.norm())
         self.template.copy_(t / t.norm())
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state_dict(self) -> dict:
+        """The tracker's state between frames as numpy arrays: this rank's particles (after the last resample, so
+        Q is zero), the template, the template box, the frame size and the frame index. The motion noise and the
+        resample word are counter-based (seed, frame index, global particle index: SPEC S1/S2), so a tracker that
+        loads this continues bit for bit."""
+        if self.pf is None:
+            raise RuntimeError("call init(frame, bbox) first")
+        return {"format": np.int64(1), "frame_index": np.int64(self.frame_index),
+                "pf_frame": np.int64(self.pf.frame), "particles": self.pf.particles.cpu().numpy(),
+                "template": self.template.cpu().numpy(), "box_wh": np.array(self.box_wh, np.float64),
+                "frame_hw": np.array([self.pf.height, self.pf.width], np.int64),
+                "P": np.int64(self.pf.P), "rank": np.int64(self.rank), "world_size": np.int64(self.world_size),
+                "seed": np.int64(self.pf.seed), "arch": np.array(self.arch.name)}
+
+    def load_state_dict(self, sd: dict) -> None:
+        if int(sd["format"]) != 1:
+            raise ValueError("unknown checkpoint format")
+        c = self.cfg
+        if (int(sd["P"]) != int(c["particles"]["num"]) or int(sd["rank"]) != self.rank
+                or int(sd["world_size"]) != self.world_size or str(sd["arch"]) != self.arch.name
+                or int(sd["seed"]) != int(c["particles"]["seed"])):
+            raise ValueError("checkpoint was written by a tracker with another configuration or rank layout")
+        H, W = (int(v) for v in sd["frame_hw"])
+        self.box_wh = tuple(float(v) for v in sd["box_wh"])
+        t = torch.from_numpy(np.ascontiguousarray(sd["template"], dtype=np.float32)).to(self.device)
+        if self.template is None or self.template.shape != t.shape:
+            self.template = t.contiguous()
+        else:
+            self.template.copy_(t)          # in place: a captured graph reads this buffer
+        if self.pf is None:
+            self.pf = ParticleFilter(int(c["particles"]["num"]), (0.0, 0.0, 1.0), c["particles"]["motion_std"],
+                                     c["particles"]["scale_range"], int(c["particles"]["seed"]), self.device, (H, W),
+                                     self.lam, self.bits, self.rank, self.world_size, self.group)
+        self.pf.reset((0.0, 0.0, 1.0))
+        self.pf.height, self.pf.width = H, W
+        self.pf.particles.copy_(torch.from_numpy(np.ascontiguousarray(sd["particles"], dtype=np.float32)))
+        self.pf.frame = int(sd["pf_frame"])
+        self.frame_index = int(sd["frame_index"])
+        self._graph = None
+
+    def save_checkpoint(self, path: str) -> str:
+        """np.savez of state_dict() (no pickled objects); with several ranks each writes `<path>.rank<r>of<G>.npz`.
+        Returns the file written."""
+        if self.world_size > 1:
+            path = f"{path}.rank{self.rank}of{self.world_size}.npz"
+        elif not path.endswith(".npz"):
+            path = path + ".npz"
+        np.savez(path, **self.state_dict())
+        return path
+
+    def load_checkpoint(self, path: str) -> None:
+        if self.world_size > 1:
+            path = f"{path}.rank{self.rank}of{self.world_size}.npz"
+        elif not path.endswith(".npz"):
+            path = path + ".npz"
+        with np.load(path, allow_pickle=False) as z:
+            self.load_state_dict({k: z[k] for k in z.files})
+
     def box(self, state) -> Tuple[float, float, float, float]:
         """(x, y, w, h) of the box a state (centre x, y, scale) stands for (SPEC S3: scale x template size)."""
         x, y, s = (float(v) for v in state)
