@@ -13,10 +13,10 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-P, FRAMES = 256, 5
+FRAMES = 5
 
 
-def _cfg():
+def _cfg(P):
     from vitparticlefiltertracker_amd import load_config
     return load_config({"model": {"arch": "vit_tiny_patch16_224", "dtype": "bf16", "weights": {"seed": 3}},
                         "particles": {"num": P, "seed": 99}})
@@ -39,7 +39,7 @@ def _run(tr, clip):
     return out
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, P, q):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -47,7 +47,7 @@ def _worker(rank, world, port, q):
     try:
         from vitparticlefiltertracker_amd import Tracker
         from vitparticlefiltertracker_amd.frames import synthetic_clip
-        tr = Tracker(_cfg(), device="cuda:0", rank=rank, world_size=world)
+        tr = Tracker(_cfg(P), device="cuda:0", rank=rank, world_size=world)
         q.put((rank, _run(tr, synthetic_clip(FRAMES + 1))))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, repr(e)))
@@ -56,15 +56,16 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_tracker_equals_single_rank(world):
+@pytest.mark.parametrize("world,P", [(2, 256), (4, 256), (3, 33)])
+def test_sharded_tracker_equals_single_rank(world, P):
+    """(3, 33): 11 particles per rank, an odd (padded) shard chunk and a world size that is not a power of two."""
     from vitparticlefiltertracker_amd import Tracker
     from vitparticlefiltertracker_amd.frames import synthetic_clip
-    ref = _run(Tracker(_cfg(), device="cuda:0"), synthetic_clip(FRAMES + 1))
+    ref = _run(Tracker(_cfg(P), device="cuda:0"), synthetic_clip(FRAMES + 1))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=300) for _ in procs)

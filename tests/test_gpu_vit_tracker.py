@@ -106,12 +106,16 @@ def test_tracker_fp32_matches_oracle_end_to_end():
         np.testing.assert_allclose(e_gpu, e_ref, rtol=1e-4)
 
 
-@pytest.mark.parametrize("use_graph,dtype,arch_name", [(True, "bf16", "vit_tiny_patch16_224"),
-                                                        (False, "bf16", "vit_tiny_patch16_224"),
-                                                        (True, "fp8", "vit_small_patch16_224")])
-def test_tracker_bf16_weight_injection_bit_exact(use_graph, dtype, arch_name):
+@pytest.mark.parametrize("use_graph,dtype,arch_name,P", [(True, "bf16", "vit_tiny_patch16_224", 256),
+                                                          (False, "bf16", "vit_tiny_patch16_224", 256),
+                                                          (True, "fp8", "vit_small_patch16_224", 256),
+                                                          (True, "bf16", "vit_base_patch16_224", 1),
+                                                          (True, "bf16", "vit_tiny_patch16_224", 37),
+                                                          (True, "fp8", "vit_small_patch16_224", 3)])
+def test_tracker_bf16_weight_injection_bit_exact(use_graph, dtype, arch_name, P):
+    """Ragged sizes too: one particle (197 GEMM rows, a single partial tile everywhere), 37 and 3 (odd shard
+    chunks, GEMM row counts that are not a multiple of the 256-row tile, CLS GEMMs of a few rows)."""
     from vitparticlefiltertracker_amd import Tracker
-    P = 256
     cfg = _tiny_cfg(P, dtype, arch_name)
     arch = ARCHS[arch_name]
     w = make_vit_weights(arch, seed=3)
