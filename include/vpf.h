@@ -85,6 +85,17 @@ int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, const float
                   const float* colsum, uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                   int epilogue, int stats_parts, float ln_eps, float* stats_out, uint8_t* C8, int64_t ld8,
                   uint32_t* Cs, int64_t lds_c, void* stream);
+/* Split-K form of vpf_gemm_bf16 for GEMMs with few rows (the last block's CLS-row GEMMs): `splits` blocks per
+ * 256 x 256 output tile each run K/splits of the K loop into fp32 partial planes (partial_ws: fp32[splits][M][N],
+ * ws_elems >= splits*M*N, 16-B aligned), then one pass sums the planes in split order and applies the epilogue.
+ * The summation order is fixed by (K, splits), never by M, so a row's result does not depend on how many rows the
+ * call has. Epilogues: VPF_EPI_BIAS, _BIAS_GELU, _BIAS_RESIDUAL (residual: C's layout, may alias C; stats_out
+ * optional, as vpf_gemm_bf16's with R = M, N % 64 == 0), _LN, _LN_GELU (row_stats = {mean, rstd} per row, colsum).
+ * Requires K % (64*splits) == 0, 1 <= splits <= 64, N % 8 == 0, lda % 8 == 0, ldc % 8 == 0, 16-B aligned A, W, C. */
+int vpf_gemm_bf16_splitk(const uint16_t* A, int64_t lda, const uint16_t* W, const float* bias,
+                         const uint16_t* residual, const float* row_stats, const float* colsum, uint16_t* C,
+                         int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue, int splits, float* stats_out,
+                         float* partial_ws, int64_t ws_elems, void* stream);
 /* Tuning knob for vpf_gemm_bf16 (process-wide; call it only between launches). kernel: 1 = the deep-ring
  * kernel (3 A + 2 B K-tiles in LDS; the product), 2 = the 2-stage ring (A/B timing; no fp8 output, <= 15
  * planes). group: A-panel group size of the tile order, also used by vpf_gemm_mx8 (0 = row-major; < 0 =

@@ -794,3 +794,55 @@ def test_estimate_resample_global(G, P, mode):
         assert np.array_equal(anc.cpu().numpy(), ref[r * n:(r + 1) * n]), f"shard {r}: ancestors"
         assert np.array_equal(st.cpu().numpy().view(np.uint32), p[:, ref[r * n:(r + 1) * n]].view(np.uint32))
         assert torch.equal(stats.cpu(), s1), f"shard {r}: statistics bits depend on G"
+
+
+@pytest.mark.parametrize("M,N,K,S", [(1, 768, 768, 3), (37, 768, 3072, 12), (512, 768, 3072, 12), (700, 3072, 768, 3),
+                                     (300, 192, 192, 1), (256, 1024, 4096, 16)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 4, 5])
+def test_gemm_splitk(M, N, K, S, epi):
+    """vpf_gemm_bf16_splitk (the last block's CLS-row GEMMs) vs an fp64 reference of the same epilogue, on
+    row-strided views (the CLS rows of a token tensor); with the residual in place and its statistics planes; and
+    a row's bits independent of the call's row count (the first rows of an M-row call equal a 1-row call)."""
+    torch.manual_seed(M + N + K + epi)
+    stride = 3 * max(N, K)                          # rows strided like the CLS rows of [n][N_tok][D]
+    Abuf = torch.randn(M, stride, device=DEV).to(torch.bfloat16)
+    A = Abuf[:, :K]
+    W = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    bias = 0.1 * torch.randn(N, device=DEV)
+    ws = torch.empty(S * M * N, device=DEV)
+    st = colsum = None
+    Rbuf = torch.randn(M, stride, device=DEV).to(torch.bfloat16)
+    out = Rbuf[:, :N] if epi == 2 else torch.empty(M, stride, device=DEV, dtype=torch.bfloat16)[:, :N]
+    R0 = Rbuf[:, :N].clone()
+    acc = A.double() @ W.double().t()
+    if epi in (4, 5):
+        st = torch.stack([torch.randn(M, device=DEV) * 0.1, 1.0 + torch.rand(M, device=DEV)], 1).contiguous()
+        colsum = W.float().sum(1)
+        acc = st[:, 1:].double() * acc - (st[:, 1:] * st[:, :1]).double() * colsum.double() + bias.double()
+    else:
+        acc = acc + bias.double()
+    planes = torch.full((N // 64, M, 2), 7.0, device=DEV) if epi == 2 and N % 64 == 0 else None
+    vpf().gemm_splitk_(A, W, bias, out if epi == 2 else None, st, colsum, epi, S, out, planes, ws)
+    if epi in (1, 5):
+        ref = Fn.gelu(acc)
+    elif epi == 2:
+        ref = acc.to(torch.bfloat16).double() + R0.double()
+    else:
+        ref = acc
+    torch.testing.assert_close(out.double(), ref, rtol=1.6e-2, atol=1.5e-2)
+    if planes is not None:
+        torch.testing.assert_close(planes.double(), _planes_ref(out, N // 64), rtol=1e-4, atol=1e-3)
+    if epi != 2:   # row invariance: the first row alone gives the same bits
+        one = torch.empty(1, N, device=DEV, dtype=torch.bfloat16)
+        vpf().gemm_splitk_(A[:1], W, bias, None, None if st is None else st[:1].contiguous(), colsum, epi, S, one,
+                           None, ws)
+        assert torch.equal(one[0], out[0])
+
+
+def test_gemm_splitk_rejects_bad_split():
+    A = torch.zeros(4, 768, device=DEV, dtype=torch.bfloat16)
+    W = torch.zeros(768, 768, device=DEV, dtype=torch.bfloat16)
+    out = torch.empty(4, 768, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(Exception):   # 768 is not a multiple of 64 * 5
+        vpf().gemm_splitk_(A, W, torch.zeros(768, device=DEV), None, None, None, 0, 5, out, None,
+                           torch.empty(5 * 4 * 768, device=DEV))

@@ -48,8 +48,10 @@ constexpr int AUX_BYTES = 2048 + AUX_PARTS * 2048;
 // math, image traffic and residual loads kept), 2 = no epilogue at all (the accumulators kept alive by an empty asm),
 // 3 = kernel 1 with a staggered start: the first workgroup on each CU sleeps phase x nk x ~1000 cycles, phase =
 // (block >> 3) mod 2^(group >> 17), so the CUs' epilogue store bursts fall in different phases of the tile period.
+// PART (vpf_gemm_bf16_splitk): blockIdx.y = split s of gridDim.y; the block runs K-tiles [s K/S, (s+1) K/S) and stores
+// its raw fp32 accumulators to the partial plane s ((float*)C + s M N, row-major [M][N]) with no epilogue.
 template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false, bool ILV = true, bool PIPED_EPI = true,
-          bool PAR = true, int LAB = 0>
+          bool PAR = true, int LAB = 0, bool PART = false>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W,
                                                         const float* __restrict__ bias,
@@ -85,8 +87,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     }
 
     // ---- per-lane DMA source offsets (bytes, relative to the block's panel base) ----
-    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * lda * 2;
-    const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2;
+    const int kbase = PART ? (int)blockIdx.y * (K / (int)gridDim.y) : 0;   // PART: this split's first K column
+    const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * lda * 2 + (size_t)kbase * 2;
+    const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2 + (size_t)kbase * 2;
     uint32_t offA[4], offB[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -162,8 +165,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     // (mean, rstd)), so their latency hides under the K loop and nothing epilogue-related stays live in
     // VGPRs across it (holding them in registers cost ~10 % on the LayerNorm-folded GEMMs: 250 VGPRs).
     // Out-of-range columns / rows read clamped (valid) addresses; their values are never stored.
-    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
-    const int nk = K / BK;
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU) && !PART;
+    const int nk = (PART ? K / (int)gridDim.y : K) / BK;
     char* aux = DEEP ? smem + (nk % 3) * OPERAND_BYTES : smem + LDS_BYTES;
     // stats_parts == 0: one {mean, rstd} plane; else stats_parts {sum, sumsq} planes of M rows each. A
     // plane's 256-row slice is 2 KiB = two 16-B-per-lane pieces (M even, 16-B aligned base), dealt round-robin
@@ -188,6 +191,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         }
     };
     auto load_aux = [&]() {
+        if constexpr (PART) return;   // no epilogue operands
         if (wid == 0)
             __builtin_amdgcn_global_load_lds((gptr_t)(bias + min(n0 + lane * 4, N - 4)), (lptr_t)aux, 16, 0, 0);
         if constexpr (LN) {
@@ -276,6 +280,22 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         }
     }
 
+    if constexpr (PART) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // the past-the-end refills land before the wave exits
+        // lane: output row m0 + wm*128 + i*16 + (lane & 15), columns n0 + wn*64 + j*16 + 4*(lane >> 4) .. +3
+        float* P = reinterpret_cast<float*>(C) + (size_t)blockIdx.y * M * N;
+        const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int m = m0 + wm * 128 + i * 16 + fr;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = n0 + wn * 64 + j * 16 + fq * 4;
+                if (m < M && n < N) *reinterpret_cast<f32x4*>(P + (size_t)m * N + n) = acc[j][i];
+            }
+        }
+        return;
+    }
     if constexpr (LAB == 2) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -1220,6 +1240,148 @@ VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, con
         case VPF_EPI_LN: VPF_GEMM_LAUNCH(VPF_EPI_LN); break;
         case VPF_EPI_LN_GELU: VPF_GEMM_LAUNCH(VPF_EPI_LN_GELU); break;
         default: return VPF_ERR_ARG;
+    }
+    VPF_RETURN_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Split-K form for GEMMs with few rows (the last block's CLS-row GEMMs: M = particles per GPU, so 6 - 48 output
+// tiles each running the whole K loop on one CU). S blocks per tile each run K/S (k_gemm_bf16<PART>) into fp32
+// partial planes; k_splitk_reduce sums the S planes in split order (fixed: the result does not depend on M) and
+// applies the epilogue with the semantics of vpf_gemm_bf16's: LN / LN_GELU from {mean, rstd} row statistics,
+// BIAS / BIAS_GELU, BIAS_RESIDUAL (bf16(acc + b) + residual, rounded again) with optional statistics planes of the
+// stored values. One thread per 8 consecutive columns of a row; a 64-column plane block is 8 lanes (xor shuffles).
+template <int EPI>
+__global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ P, int S, int M, int N,
+                                                       const float* __restrict__ bias,
+                                                       const float2* __restrict__ stats,
+                                                       const float* __restrict__ colsum, const bf16_t* residual,
+                                                       bf16_t* C, int64_t ldc, float* stats_out) {
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    constexpr bool GELU = (EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU);
+    const int per_row = N >> 3;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = t < (int64_t)M * per_row;
+    const int m = live ? (int)(t / per_row) : 0;
+    const int n = live ? (int)(t - (int64_t)m * per_row) * 8 : 0;
+    float v[8];
+    if (live) {
+        const float* p = P + (size_t)m * N + n;
+        const float4 a0 = *reinterpret_cast<const float4*>(p), a1 = *reinterpret_cast<const float4*>(p + 4);
+        v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+        for (int s = 1; s < S; ++s) {
+            const float* q = p + (size_t)s * M * N;
+            const float4 b0 = *reinterpret_cast<const float4*>(q), b1 = *reinterpret_cast<const float4*>(q + 4);
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+        float rstd = 1.f, nrm = 0.f;
+        if constexpr (LN) {
+            const float2 st = stats[m];
+            rstd = st.y;
+            nrm = -st.y * st.x;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float y = LN ? fmaf(rstd, v[e], fmaf(nrm, colsum[n + e], bias[n + e])) : v[e] + bias[n + e];
+            if constexpr (GELU) {
+                const f32x2 g = gelu_sig2(f32x2{y, y});
+                y = g.x;
+            }
+            v[e] = y;
+        }
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack_bf2(v[2 * e], v[2 * e + 1]);
+    if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) {
+        if (live) {
+            const uint4 rv = *reinterpret_cast<const uint4*>(residual + (size_t)m * ldc + n);
+            const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = pack_bf2(bf2f((bf16_t)(o[e] & 0xffff)) + bf2f((bf16_t)(rr[e] & 0xffff)),
+                                bf2f((bf16_t)(o[e] >> 16)) + bf2f((bf16_t)(rr[e] >> 16)));
+        }
+        if (stats_out != nullptr) {   // {sum, sumsq} of the stored values over this lane's 64-column block
+            float s1 = 0.f, s2 = 0.f;
+            if (live) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float lo = bf2f((bf16_t)(o[e] & 0xffff)), hi = bf2f((bf16_t)(o[e] >> 16));
+                    s1 += lo + hi;
+                    s2 = fmaf(lo, lo, s2);
+                    s2 = fmaf(hi, hi, s2);
+                }
+            }
+#pragma unroll
+            for (int x = 1; x < 8; x <<= 1) {
+                s1 += __shfl_xor(s1, x, 64);
+                s2 += __shfl_xor(s2, x, 64);
+            }
+            if (live && (n & 63) == 0)
+                *reinterpret_cast<float2*>(stats_out + ((int64_t)(n >> 6) * M + m) * 2) = make_float2(s1, s2);
+        }
+    }
+    if (live) *reinterpret_cast<uint4*>(C + (size_t)m * ldc + n) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+VPF_API int vpf_gemm_bf16_splitk(const uint16_t* A, int64_t lda, const uint16_t* W, const float* bias,
+                                 const uint16_t* residual, const float* row_stats, const float* colsum, uint16_t* C,
+                                 int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue, int splits,
+                                 float* stats_out, float* partial_ws, int64_t ws_elems, void* stream) {
+    if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || K % ((int64_t)splits * BK) != 0 || N % 8 != 0 || lda < K ||
+        lda % 8 != 0 || ldc < N || ldc % 8 != 0)
+        return VPF_ERR_ARG;
+    if (M > INT32_MAX / 2 || N > 65536 || K > 65536 || lda > INT32_MAX / 2 || ldc > INT32_MAX / 2 || splits > 64)
+        return VPF_ERR_ARG;
+    if ((uint64_t)BM * (uint64_t)lda * 2 > UINT32_MAX) return VPF_ERR_ARG;
+    if (!A || !W || !bias || !C || !partial_ws || ws_elems < (int64_t)splits * M * N) return VPF_ERR_ARG;
+    if (((uintptr_t)partial_ws & 15) || ((uintptr_t)C & 15) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15))
+        return VPF_ERR_ARG;
+    const bool ln = epilogue == VPF_EPI_LN || epilogue == VPF_EPI_LN_GELU;
+    if (ln && (!row_stats || !colsum || ((uintptr_t)row_stats & 7))) return VPF_ERR_ARG;
+    if (epilogue == VPF_EPI_BIAS_RESIDUAL && (!residual || ((uintptr_t)residual & 15))) return VPF_ERR_ARG;
+    if (stats_out && (epilogue != VPF_EPI_BIAS_RESIDUAL || N % 64 != 0 || ((uintptr_t)stats_out & 7)))
+        return VPF_ERR_ARG;
+    if (epilogue != VPF_EPI_BIAS && epilogue != VPF_EPI_BIAS_GELU && epilogue != VPF_EPI_BIAS_RESIDUAL && !ln)
+        return VPF_ERR_ARG;
+    const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (tiles > 65535 * 256) return VPF_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const int m = (int)M, n = (int)N, k = (int)K;
+    const Out8 o8{nullptr, nullptr, 0, 0};
+    hipLaunchKernelGGL((k_gemm_bf16<VPF_EPI_BIAS, true, false, false, true, true, true, 0, true>),
+                       dim3((unsigned)tiles, (unsigned)splits), dim3(NTHREADS), 0, s, reinterpret_cast<const bf16_t*>(A),
+                       (int)lda, reinterpret_cast<const bf16_t*>(W), nullptr, nullptr, nullptr, 1, nullptr, nullptr,
+                       reinterpret_cast<bf16_t*>(partial_ws), n, m, n, k, tile_group(), 0, 0.f, nullptr, m, o8);
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+    const int64_t threads = M * (N / 8);
+    const dim3 rg((unsigned)((threads + 255) / 256));
+    const float2* st = reinterpret_cast<const float2*>(row_stats);
+    const bf16_t* R = reinterpret_cast<const bf16_t*>(residual);
+    bf16_t* Cb = reinterpret_cast<bf16_t*>(C);
+    switch (epilogue) {
+        case VPF_EPI_BIAS:
+            hipLaunchKernelGGL(k_splitk_reduce<VPF_EPI_BIAS>, rg, dim3(256), 0, s, partial_ws, splits, m, n, bias, st,
+                               colsum, R, Cb, ldc, nullptr);
+            break;
+        case VPF_EPI_BIAS_GELU:
+            hipLaunchKernelGGL(k_splitk_reduce<VPF_EPI_BIAS_GELU>, rg, dim3(256), 0, s, partial_ws, splits, m, n, bias,
+                               st, colsum, R, Cb, ldc, nullptr);
+            break;
+        case VPF_EPI_BIAS_RESIDUAL:
+            hipLaunchKernelGGL(k_splitk_reduce<VPF_EPI_BIAS_RESIDUAL>, rg, dim3(256), 0, s, partial_ws, splits, m, n,
+                               bias, st, colsum, R, Cb, ldc, stats_out);
+            break;
+        case VPF_EPI_LN:
+            hipLaunchKernelGGL(k_splitk_reduce<VPF_EPI_LN>, rg, dim3(256), 0, s, partial_ws, splits, m, n, bias, st,
+                               colsum, R, Cb, ldc, nullptr);
+            break;
+        default:
+            hipLaunchKernelGGL(k_splitk_reduce<VPF_EPI_LN_GELU>, rg, dim3(256), 0, s, partial_ws, splits, m, n, bias,
+                               st, colsum, R, Cb, ldc, nullptr);
+            break;
     }
     VPF_RETURN_LAUNCH();
 }

@@ -163,6 +163,35 @@ def gemm_stats_(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: 
     _gemm(a, w, bias, residual, pos, patch_rows, None, None, epilogue, out, 0, 0.0, stats_out)
 
 
+@torch.library.custom_op("vpf::gemm_splitk_", mutates_args={"out", "stats_out", "ws"}, device_types="cuda")
+def gemm_splitk_(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: Optional[torch.Tensor],
+                 row_stats: Optional[torch.Tensor], colsum: Optional[torch.Tensor], epilogue: int, splits: int,
+                 out: torch.Tensor, stats_out: Optional[torch.Tensor], ws: torch.Tensor) -> None:
+    """Split-K bf16 GEMM (vpf_gemm_bf16_splitk) for few-row GEMMs: `splits` K-chunks into the fp32 workspace `ws`
+    (>= splits*M*N), summed in split order, then the epilogue (BIAS, BIAS_GELU, BIAS_RESIDUAL [+ stats_out planes
+    [N/64][M][2]], LN / LN_GELU with {mean, rstd} row_stats). `a`, `out`, `residual` may be row-strided views."""
+    _dev(w, bias, row_stats, colsum, stats_out, ws)
+    for t in (a, out, residual):
+        if t is not None:
+            _chk(t.is_cuda, "vpf ops run on the GPU only (no CPU fallback); got a CPU tensor")
+    M, lda = _rows(a, "gemm_splitk a")
+    K, N = a.shape[1], w.shape[0]
+    _chk(a.dtype == w.dtype == out.dtype == _BF16, "gemm_splitk: bf16 operands")
+    _chk(w.shape[1] == K and bias.numel() == N and bias.dtype == _F32, "gemm_splitk: shape mismatch")
+    Mo, ldc = _rows(out, "gemm_splitk out")
+    _chk(Mo == M and out.shape[1] == N, "gemm_splitk: output shape")
+    if residual is not None:
+        _chk(_rows(residual, "gemm_splitk residual") == (M, ldc), "gemm_splitk: residual must match out's layout")
+    if epilogue in (_lib.VPF_EPI_LN, _lib.VPF_EPI_LN_GELU):
+        _chk(row_stats is not None and row_stats.numel() >= 2 * M and colsum is not None and colsum.numel() == N,
+             "gemm_splitk: LN epilogue needs {mean, rstd} row_stats [M][2] and colsum[N]")
+    if stats_out is not None:
+        _chk(stats_out.dtype == _F32 and stats_out.numel() >= (N // 64) * M * 2, "gemm_splitk: stats_out [N/64][M][2]")
+    _chk(ws.dtype == _F32 and ws.numel() >= splits * M * N, "gemm_splitk: workspace f32[splits*M*N]")
+    call("vpf_gemm_bf16_splitk", ptr(a), lda, ptr(w), ptr(bias), ptr(residual), ptr(row_stats), ptr(colsum), ptr(out),
+         ldc, M, N, K, epilogue, splits, ptr(stats_out), ptr(ws), ws.numel(), stream_ptr())
+
+
 # ---------------------------------------------------------------------------------------------- MX8 (fp8 path)
 # An MX8 tensor is a pair (q, s): q uint8[rows][K] (e4m3fn codes; a row-strided view is allowed) and s int32
 # [K/128][lds] scale planes (e8m0 bytes in 64-row bricks, vpf.h "MX8 operands"), lds = rows rounded up to 64.

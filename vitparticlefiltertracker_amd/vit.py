@@ -52,6 +52,14 @@ def norm_affine(mean, std):
     return a + b
 
 
+def _splits(K: int) -> int:
+    """K-chunks of the split-K CLS-row GEMMs: ~256 deep each (the largest s <= K / 256 with K % (64 s) == 0)."""
+    s = max(1, K // 256)
+    while K % (64 * s):
+        s -= 1
+    return s
+
+
 class KernelTimer:
     """HIP-event timing of individual launches on the current stream (eager mode only; bench.py)."""
 
@@ -211,6 +219,8 @@ class ViTEngine:
         if self.cls_fused:
             self.clsG = torch.empty(n, A.heads * D, device=dev, dtype=dt)
             self.clsU = torch.empty(n, A.heads * D, device=dev, dtype=dt)
+        if self.fold_ln:   # split-K partial planes of the last block's CLS-row GEMMs (q, proj, fc2)
+            self.splitk_ws = torch.empty(n * D * max(_splits(D), _splits(F)), device=dev, dtype=torch.float32)
         self.Q = torch.empty(n, device=dev, dtype=torch.int64)
         self.feat = torch.empty(n, D, device=dev, dtype=torch.float32)
         self.sim = torch.empty(n, device=dev, dtype=torch.float32)
@@ -301,6 +311,17 @@ class ViTEngine:
         fold, planes = self.fold_ln, self.use_planes
         P, eps = self.parts, A.ln_eps
         pl = self.planes(n) if planes else None                # planes of h2 (written by embed / proj / fc2)
+        ws = self.splitk_ws if fold else None
+        sk = fold and os.environ.get("VPF_CLS_SPLITK", "1") != "0"   # 0: the one-pass kernel (A/B timing)
+
+        def q_cls():
+            """The CLS rows' LN-folded query (row statistics from the row_stats pass in stc)."""
+            if sk:
+                _run(T, "gemm_q_cls", vpf.gemm_splitk_, hc, L["wqkv"][:D], L["bqkv"][:D], None, stc, L["cqkv"][:D],
+                     LNE, _splits(D), qc, None, ws)
+            else:
+                _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc, L["cqkv"][:D],
+                     LNE, qc)
         plc = self.planes_cls_flat[: P * n * 2].view(P, n, 2)  # planes of the last block's CLS rows
 
         def ln_stats(x, st_rows, pln):
@@ -361,8 +382,7 @@ class ViTEngine:
                 elif self.cls_fused:
                     # K, V never formed: the CLS query, G = W'_k^T q per head, the folded attention, then W'_v
                     _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # the CLS rows' {mean, rstd}
-                    _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc,
-                         L["cqkv"][:D], LNE, qc)
+                    q_cls()
                     G, U = self.clsG[:n], self.clsU[:n]
                     _run(T, "gemm_cls_g", vpf.gemm, qc, self.w_clsG, self.b_clsG, None, None, 0, None, None, BIAS, G)
                     _run(T, "attention_cls", vpf.cls_attn_fold_, self.h[:n], pl, eps, G, qc, L["bqkv"][D:2 * D],
@@ -376,14 +396,12 @@ class ViTEngine:
                     _run(T, "gemm_kv", vpf.gemm_mx8, h8q, h8s, *L["wkv8"], L["bqkv"][D:], None, s8, L["cqkv8"][D:],
                          LNE, kv2, p8, eps)
                     _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # the CLS rows' {mean, rstd}
-                    _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc,
-                         L["cqkv"][:D], LNE, qc)
+                    q_cls()
                 else:
                     _run(T, "gemm_kv", vpf.gemm, h2, L["wqkv"][D:], L["bqkv"][D:], None, None, 0, s1, L["cqkv"][D:],
                          LNE, kv2, p1, eps)
                     _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # the CLS rows' {mean, rstd}
-                    _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc,
-                         L["cqkv"][:D], LNE, qc)
+                    q_cls()
             else:
                 _run(T, "layernorm", vpf.layernorm, h2, L["n1g"], L["n1b"], A.ln_eps, x2)
                 if not last:
@@ -398,7 +416,19 @@ class ViTEngine:
                      self.x[:n])
             hh, xx, hd_, ss, pp = (hc, xc, hidc, stc, plc) if last else (h2, x2, hid, st, pl)
             tag = "_cls" if last else ""
-            if fold:
+            if fold and last and sk:
+                # the CLS rows (n of them): split-K proj / fc2 (a few output tiles each running the whole K loop on
+                # one CU otherwise; fixed split order, so a row's result does not depend on n); fc1 has 4x the
+                # tiles and stays on the one-pass kernel
+                _run(T, "gemm_proj" + tag, vpf.gemm_splitk_, xx, L["wproj"], L["bproj"], hh, None, None, RES,
+                     _splits(D), hh, pp if planes else None, ws)
+                s2, p2 = ln_stats(hh, ss, pp)
+                _run(T, "gemm_fc1" + tag, vpf.gemm, hh, L["wfc1"], L["bfc1"], None, None, 0, s2, L["cfc1"], LNG, hd_,
+                     p2, eps)
+                # the last block's output only feeds the final LayerNorm (cls_weight computes its own stats)
+                _run(T, "gemm_fc2" + tag, vpf.gemm_splitk_, hd_, L["wfc2"], L["bfc2"], hh, None, None, RES, _splits(F),
+                     hh, None, ws)
+            elif fold:
                 residual_gemm("gemm_proj" + tag, xx, L["wproj"], L["bproj"], hh, pp)
                 s2, p2 = ln_stats(hh, ss, pp)
                 _run(T, "gemm_fc1" + tag, vpf.gemm, hh, L["wfc1"], L["bfc1"], None, None, 0, s2, L["cfc1"], LNG, hd_,
