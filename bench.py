@@ -168,6 +168,9 @@ def main() -> int:
             dist.init_process_group("gloo")
     if args.particles % world:
         raise SystemExit("--particles must be divisible by the number of ranks")
+    if args.gpus != world and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 ranks with "
+              "python -m torch.distributed.run --nproc-per-node N ... (measuring the ranks that exist)", file=sys.stderr)
 
     from vitparticlefiltertracker_amd import Tracker, load_config
     from vitparticlefiltertracker_amd.config import ARCHS
