@@ -50,7 +50,8 @@ def main(argv=None) -> int:
     if args.resume:
         tr.load_checkpoint(args.resume)
         for _ in range(tr.frame_index):       # frames 1 .. frame_index were tracked before the checkpoint
-            next(frames)
+            if next(frames, None) is None:
+                raise SystemExit(f"--resume: the checkpoint is at frame {tr.frame_index}, past the end of the input")
         start = tr.frame_index + 1
     else:
         tr.init(first, inp["bbox0"])
