@@ -139,3 +139,25 @@ def test_oracle_weights_clamp_and_nonfinite():
     assert q[0] == q[1] == q[2] == 2 ** 40
     assert q[3] == q[4] == q[5] == 0
     assert 0 < q[6] < q[7] < 2 ** 40
+
+
+def test_c_abi_rejects_bad_shapes_before_any_launch():
+    """The C-ABI validates shapes on the host and returns VPF_ERR_ARG (-1) without touching the device (this
+    runs without a GPU): the device-resident estimate/resample and the split-K GEMM."""
+    from vitparticlefiltertracker_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    L = _lib.lib()
+    fake = 4096                                          # never dereferenced: validation fails first
+    er = L.vpf_estimate_resample
+    # P = 0; P not a multiple of the shard; slot range past P; shard strides too short for several shards
+    assert er(fake, 8, fake, 8, 24, 8, 0, 1, 1, 0, 0, fake, fake, 8, fake, fake, None) == -1
+    assert er(fake, 8, fake, 8, 24, 7, 16, 1, 1, 0, 8, fake, fake, 8, fake, fake, None) == -1
+    assert er(fake, 8, fake, 8, 24, 8, 16, 1, 1, 8, 17, fake, fake, 9, fake, fake, None) == -1
+    assert er(fake, 4, fake, 8, 24, 8, 16, 1, 1, 0, 8, fake, fake, 8, fake, fake, None) == -1
+    assert er(fake, 8, fake, 8, 20, 8, 16, 1, 1, 0, 8, fake, fake, 8, fake, fake, None) == -1
+    sk = L.vpf_gemm_bf16_splitk
+    # K = 768 not a multiple of 64 * 5 splits; workspace too small; LN without row statistics
+    assert sk(fake, 768, fake, fake, None, None, None, fake, 768, 4, 768, 768, 0, 5, None, fake, 10 ** 7, None) == -1
+    assert sk(fake, 768, fake, fake, None, None, None, fake, 768, 4, 768, 768, 0, 3, None, fake, 100, None) == -1
+    assert sk(fake, 768, fake, fake, None, None, None, fake, 768, 4, 768, 768, 4, 3, None, fake, 10 ** 7, None) == -1
