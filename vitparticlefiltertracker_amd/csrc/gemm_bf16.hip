@@ -1162,9 +1162,22 @@ static int gemm_cus() {   // compute units of the current device (the persistent
 }
 
 static int g_group = -1;
+static bool g_group_set = false;   // VPF_GEMM_GROUP or vpf_gemm_tune set one group for every shape
 static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size of the tile order (0 = tm-major)
-    if (g_group < 0) { const char* e = getenv("VPF_GEMM_GROUP"); g_group = e ? atoi(e) : 4; if (g_group < 0) g_group = 0; }
+    if (g_group < 0) {
+        const char* e = getenv("VPF_GEMM_GROUP");
+        g_group = e ? atoi(e) : 4;
+        g_group_set = e != nullptr;
+        if (g_group < 0) g_group = 0;
+    }
     return g_group;
+}
+// Default group per shape (profiles/r2_gemm_lab/group_sweep_r2.txt, one process): the N <= 1024 GEMMs (proj / FC2:
+// 3 column tiles, so a group of 4 A panels keeps 12 tiles of one K panel set in flight) are 1-1.5 % faster with 2
+// panels per group (FC2 3.196 vs 3.226 ms, proj 1.070 vs 1.082), QKV / FC1 with 4. The order never changes a bit.
+static int tile_group_for(int64_t N) {
+    const int g = tile_group();
+    return g_group_set ? g : (N <= 1024 ? 2 : g);
 }
 
 // GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, refills issued from the MFMA block (product);
@@ -1182,7 +1195,7 @@ int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
 VPF_API int vpf_gemm_tune(int kernel, int group) {
     if (kernel < 1 || kernel > 16) return VPF_ERR_ARG;
     g_kernel = kernel;
-    if (group >= 0) { tile_group(); g_group = group; }
+    if (group >= 0) { tile_group(); g_group = group; g_group_set = true; }
     return 0;
 }
 
@@ -1230,7 +1243,7 @@ VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, con
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)tiles), block(NTHREADS);
     const int kern = gemm_kernel();
-    const int group = tile_group();
+    const int group = tile_group_for(N);
     const int m = (int)M, n = (int)N, k = (int)K;
     switch (epilogue) {
         case VPF_EPI_BIAS: VPF_GEMM_LAUNCH(VPF_EPI_BIAS); break;
