@@ -269,14 +269,14 @@ def test_gemm_kernel_variants_bit_identical(M, N, K):
         for epi in (0, 1, 2, 4, 5):
             assert L.vpf_gemm_tune(1, -1) == 0
             ref, ref_st = run(epi)
-            for k in (2, 3, 4, 5, 6, 7, 10, 13, 16):
+            for k in (0, 2, 3, 4, 5, 6, 7, 10, 13, 16):   # 0: the per-shape defaults the product runs
                 assert L.vpf_gemm_tune(k, -1) == 0
                 got, st = run(epi)
                 assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (k, epi)
                 if ref_st is not None:
                     assert torch.equal(st, ref_st), (k, epi)
     finally:
-        L.vpf_gemm_tune(1, -1)
+        L.vpf_gemm_tune(0, -1)                # the per-shape defaults
 
 
 @pytest.mark.parametrize("M,N,K", [(20000, 1000, 768), (70001, 2304, 128), (806912 // 8, 3072, 768)])
@@ -315,7 +315,7 @@ def test_gemm_persistent_bit_identical(M, N, K):
                 bad = (got.view(torch.int16) != ref.view(torch.int16)).sum().item()
                 assert bad == 0, (k, epi, bad)
     finally:
-        L.vpf_gemm_tune(1, -1)
+        L.vpf_gemm_tune(0, -1)                # the per-shape defaults
 
 
 def test_patch_and_cls_stats_planes():

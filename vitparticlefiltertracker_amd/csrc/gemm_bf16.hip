@@ -1187,15 +1187,36 @@ static int tile_group_for(int64_t N) {
 // with a staggered start in 4 / 2 / 8 phases, 13 = the persistent k_gemm_pt (LN / LN_GELU / BIAS / BIAS_GELU; else 1).
 // VPF_GEMM_KERNEL sets the initial value, vpf_gemm_tune() the current one.
 static int g_kernel = -1;
+static bool g_kernel_set = false;   // VPF_GEMM_KERNEL or vpf_gemm_tune chose one kernel for every shape
 static int gemm_kernel() {
-    if (g_kernel < 0) { const char* e = getenv("VPF_GEMM_KERNEL"); g_kernel = e ? atoi(e) : 1; if (g_kernel < 1 || g_kernel > 16) g_kernel = 1; }
+    if (g_kernel < 0) {
+        const char* e = getenv("VPF_GEMM_KERNEL");
+        g_kernel = e ? atoi(e) : 1;
+        g_kernel_set = e != nullptr;
+        if (g_kernel < 1 || g_kernel > 16) g_kernel = 1;
+    }
     return g_kernel;
+}
+// Default kernel per epilogue: the LN-folded bias-only GEMM (QKV) runs the ping-pong loop k_gemm_pp (kernel 5), 2.5 %
+// faster there in one process (2.603 vs 2.670 ms, profiles/r2_gemm_lab/kernel_ab_r2s5.txt) and bit-identical to
+// kernel 1 (test_gemm_kernel_variants_bit_identical); every other epilogue is fastest on kernel 1.
+static int gemm_kernel_for(int epilogue) {
+    const int k = gemm_kernel();
+    return g_kernel_set ? k : (epilogue == VPF_EPI_LN ? 5 : k);
 }
 int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
 VPF_API int vpf_gemm_tune(int kernel, int group) {
-    if (kernel < 1 || kernel > 16) return VPF_ERR_ARG;
+    if (kernel < 0 || kernel > 16) return VPF_ERR_ARG;
+    gemm_kernel();
+    tile_group();
+    if (kernel == 0) {   // back to the per-shape defaults (kernel and group)
+        g_kernel = 1; g_kernel_set = false;
+        g_group = 4; g_group_set = false;
+        return 0;
+    }
     g_kernel = kernel;
-    if (group >= 0) { tile_group(); g_group = group; g_group_set = true; }
+    g_kernel_set = true;
+    if (group >= 0) { g_group = group; g_group_set = true; }
     return 0;
 }
 
@@ -1242,7 +1263,7 @@ VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, con
     if (tiles > INT32_MAX) return VPF_ERR_ARG;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)tiles), block(NTHREADS);
-    const int kern = gemm_kernel();
+    const int kern = gemm_kernel_for(epilogue);
     const int group = tile_group_for(N);
     const int m = (int)M, n = (int)N, k = (int)K;
     switch (epilogue) {
