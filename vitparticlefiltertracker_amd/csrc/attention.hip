@@ -350,8 +350,13 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // (8 waves, 7 strips at N = 197) only move data and keep the barrier count. N <= 256 (one strip per wave).
 // CPB: 32-key chunks per counted wait + barrier. Waiting for 4 chunks at a time (2 barriers at N = 197)
 // measured 3-4 % faster than per-chunk barriers (1, 2, 3, 4: 1.223 / 1.210 / 1.196 / 1.178 ms at 4096 x 12
-// heads, profiles/r1_gemm_lab/attn_cpb.txt): each barrier puts all 8 waves back in lockstep.
-constexpr int PIPE_CPB = 4;
+// heads, profiles/r1_gemm_lab/attn_cpb.txt): each barrier puts all 8 waves back in lockstep. Round 2 on the current
+// kernel (profiles/r2_gemm_lab/attn_cpb_r2s5.txt, per-launch averages from bench.py): CPB 3 / 4 / 5 / 6 / 7 =
+// 1.084 / 1.075 / 1.069 / 1.064 / 1.156 ms at N = 197; 6 and 4 are level on ViT-L (N = 577) and on the MX8 output.
+#ifndef VPF_ATTN_CPB
+#define VPF_ATTN_CPB 6   // -DVPF_ATTN_CPB=n builds A/B variants (tools/ab_libs.sh)
+#endif
+constexpr int PIPE_CPB = VPF_ATTN_CPB;
 // OUT8: the output is written as MX8 (the fp8 path's proj A operand) instead of bf16: the same packed bf16
 // values, quantised per 32-dim block (a block = 16 dims of a lane + 16 of its partner half-wave lane).
 template <int CPB, bool OUT8 = false, bool TAIL8 = true>
