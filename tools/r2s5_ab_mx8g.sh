@@ -1,0 +1,11 @@
+set -o pipefail
+OUT=gpurun_out/r2s5_ab_mx8g; mkdir -p $OUT
+timeout -k 10 600 python tools/gemm_ab.py 9 qkv 5:2,5:4,5:8,5:16 > $OUT/pp_group.log 2>&1 || exit $?
+grep median $OUT/pp_group.log
+for rep in 1 2 3; do
+  for g in def 4; do
+    if [ $g = def ]; then unset VPF_GEMM_GROUP; else export VPF_GEMM_GROUP=$g; fi
+    timeout -k 10 300 python bench.py --dtype fp8 --steps 5 --warmup 2 --cpu-seconds 0 --kernel-frames 2 > $OUT/g${g}_r$rep.log 2>&1 || exit $?
+    echo "fp8 group=$g rep=$rep $(tail -1 $OUT/g${g}_r$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); k=d["kernels"]; print(d["ms_per_step"], " ".join("%s %.4f" % (n, k[n]["avg_ms"]) for n in ("gemm_qkv","gemm_proj","gemm_fc1","gemm_fc2")))')"
+  done
+done

@@ -1205,6 +1205,12 @@ static int gemm_kernel_for(int epilogue) {
     return g_kernel_set ? k : (epilogue == VPF_EPI_LN ? 5 : k);
 }
 int vpf_gemm_tile_group() { return tile_group(); }   // shared with gemm_mx8.hip
+// MX8 GEMMs' default group (profiles/r2_gemm_lab/mx8_group_sweep.txt, fp8 frames): the LN-folded bias-only QKV is ~5 %
+// faster with 8 A panels per group (1.93-1.95 vs 2.05 ms); proj / FC1 / FC2 keep 4.
+int vpf_gemm_tile_group_mx8(int epilogue) {
+    const int g = tile_group();
+    return g_group_set ? g : (epilogue == VPF_EPI_LN ? 8 : g);
+}
 VPF_API int vpf_gemm_tune(int kernel, int group) {
     if (kernel < 0 || kernel > 16) return VPF_ERR_ARG;
     gemm_kernel();

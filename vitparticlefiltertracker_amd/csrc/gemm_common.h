@@ -7,6 +7,7 @@
 
 // host helpers defined in gemm_bf16.hip, shared with gemm_mx8.hip
 int vpf_gemm_tile_group();
+int vpf_gemm_tile_group_mx8(int epilogue);
 int vpf_check_out8(const uint8_t* C8, int64_t ld8, const uint32_t* Cs, int64_t lds_c, int64_t rows, int64_t N);
 
 namespace vpf {

@@ -312,7 +312,7 @@ VPF_API int vpf_gemm_mx8(const uint8_t* A, int64_t lda, const uint32_t* As, int6
     if (tiles > INT32_MAX) return VPF_ERR_ARG;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)tiles), block(NTHREADS);
-    const int group = vpf_gemm_tile_group();
+    const int group = vpf_gemm_tile_group_mx8(epilogue);
     // VPF_MX8_VARIANT=0: the previous schedule (all MFMAs after the buffer-release barrier), for A/B timing
     const char* var = getenv("VPF_MX8_VARIANT");
     const bool late = var && var[0] == '0';
