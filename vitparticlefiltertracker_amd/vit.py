@@ -53,8 +53,10 @@ def norm_affine(mean, std):
 
 
 def _splits(K: int) -> int:
-    """K-chunks of the split-K CLS-row GEMMs: ~256 deep each (the largest s <= K / 256 with K % (64 s) == 0)."""
-    s = max(1, K // 256)
+    """K-chunks of the split-K CLS-row fc2: ~768 deep each (the largest s <= K / 768 with K % (64 s) == 0). Deeper
+    chunks would leave the 512-row case latency-bound, shallower ones cost more partial-plane traffic than they save
+    at 4096-8192 rows (profiles/r2_gemm_lab/cls_splitk_depth.txt)."""
+    s = max(1, K // 768)
     while K % (64 * s):
         s -= 1
     return s
@@ -220,7 +222,7 @@ class ViTEngine:
             self.clsG = torch.empty(n, A.heads * D, device=dev, dtype=dt)
             self.clsU = torch.empty(n, A.heads * D, device=dev, dtype=dt)
         if self.fold_ln:   # split-K partial planes of the last block's CLS-row GEMMs (q, proj, fc2)
-            self.splitk_ws = torch.empty(n * D * max(_splits(D), _splits(F)), device=dev, dtype=torch.float32)
+            self.splitk_ws = torch.empty(n * D * _splits(F), device=dev, dtype=torch.float32)
         self.Q = torch.empty(n, device=dev, dtype=torch.int64)
         self.feat = torch.empty(n, D, device=dev, dtype=torch.float32)
         self.sim = torch.empty(n, device=dev, dtype=torch.float32)
@@ -316,12 +318,8 @@ class ViTEngine:
 
         def q_cls():
             """The CLS rows' LN-folded query (row statistics from the row_stats pass in stc)."""
-            if sk:
-                _run(T, "gemm_q_cls", vpf.gemm_splitk_, hc, L["wqkv"][:D], L["bqkv"][:D], None, stc, L["cqkv"][:D],
-                     LNE, _splits(D), qc, None, ws)
-            else:
-                _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc, L["cqkv"][:D],
-                     LNE, qc)
+            _run(T, "gemm_q_cls", vpf.gemm, hc, L["wqkv"][:D], L["bqkv"][:D], None, None, 0, stc, L["cqkv"][:D],
+                 LNE, qc)
         plc = self.planes_cls_flat[: P * n * 2].view(P, n, 2)  # planes of the last block's CLS rows
 
         def ln_stats(x, st_rows, pln):
@@ -417,11 +415,10 @@ class ViTEngine:
             hh, xx, hd_, ss, pp = (hc, xc, hidc, stc, plc) if last else (h2, x2, hid, st, pl)
             tag = "_cls" if last else ""
             if fold and last and sk:
-                # the CLS rows (n of them): split-K proj / fc2 (a few output tiles each running the whole K loop on
-                # one CU otherwise; fixed split order, so a row's result does not depend on n); fc1 has 4x the
-                # tiles and stays on the one-pass kernel
-                _run(T, "gemm_proj" + tag, vpf.gemm_splitk_, xx, L["wproj"], L["bproj"], hh, None, None, RES,
-                     _splits(D), hh, pp if planes else None, ws)
+                # the CLS rows (n of them): split-K fc2 (K = MLP: a few output tiles each running the whole K loop on
+                # one CU otherwise; fixed split order, so a row's result does not depend on n). q / proj / fc1
+                # (K = D) gain nothing from splitting at 512 rows and lose at 4096-8192 (the partial planes)
+                residual_gemm("gemm_proj" + tag, xx, L["wproj"], L["bproj"], hh, pp)
                 s2, p2 = ln_stats(hh, ss, pp)
                 _run(T, "gemm_fc1" + tag, vpf.gemm, hh, L["wfc1"], L["bfc1"], None, None, 0, s2, L["cfc1"], LNG, hd_,
                      p2, eps)
