@@ -1175,9 +1175,12 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
 // Default group per shape (profiles/r2_gemm_lab/group_sweep_r2.txt, one process): the N <= 1024 GEMMs (proj / FC2:
 // 3 column tiles, so a group of 4 A panels keeps 12 tiles of one K panel set in flight) are 1-1.5 % faster with 2
 // panels per group (FC2 3.196 vs 3.226 ms, proj 1.070 vs 1.082), QKV / FC1 with 4. The order never changes a bit.
+// The N >= 3072 GEMM (FC1: 12 column tiles, W' = 4.7 MB, more than one XCD's 4 MiB L2) takes 16 A panels per group:
+// its time is flat in the group size (4.103 ms at 16 vs 4.114 at 4) but W is re-streamed from beyond L2 once per
+// group, so 16 panels cut those re-reads 4x (profiles/r2_gemm_lab/fc1_group16_pmc.txt).
 static int tile_group_for(int64_t N) {
     const int g = tile_group();
-    return g_group_set ? g : (N <= 1024 ? 2 : g);
+    return g_group_set ? g : (N <= 1024 ? 2 : N >= 3072 ? 16 : g);
 }
 
 // GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, refills issued from the MFMA block (product);
