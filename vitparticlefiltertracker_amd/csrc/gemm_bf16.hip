@@ -1175,12 +1175,14 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
 // Default group per shape (profiles/r2_gemm_lab/group_sweep_r2.txt, one process): the N <= 1024 GEMMs (proj / FC2:
 // 3 column tiles, so a group of 4 A panels keeps 12 tiles of one K panel set in flight) are 1-1.5 % faster with 2
 // panels per group (FC2 3.196 vs 3.226 ms, proj 1.070 vs 1.082), QKV / FC1 with 4. The order never changes a bit.
-// The N >= 3072 GEMM (FC1: 12 column tiles, W' = 4.7 MB, more than one XCD's 4 MiB L2) takes 16 A panels per group:
-// its time is flat in the group size (4.103 ms at 16 vs 4.114 at 4) but W is re-streamed from beyond L2 once per
-// group, so 16 panels cut those re-reads 4x (profiles/r2_gemm_lab/fc1_group16_pmc.txt).
-static int tile_group_for(int64_t N) {
+// FC1 (EPI_LN_GELU; 12 column tiles at ViT-B) takes 16 A panels per group: -0.9 % on FC1 and the frame -0.7 % in a
+// same-box A/B, although its memory-side requests go up (the extra A re-reads hit the Infinity Cache;
+// profiles/r2_gemm_lab/fc1_group16_pmc.txt).
+static int tile_group_for(int64_t N, int epilogue) {
     const int g = tile_group();
-    return g_group_set ? g : (N <= 1024 ? 2 : N >= 3072 ? 16 : g);
+    if (g_group_set) return g;
+    if (N <= 1024) return 2;
+    return epilogue == VPF_EPI_LN_GELU ? 16 : g;
 }
 
 // GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, refills issued from the MFMA block (product);
@@ -1273,7 +1275,7 @@ VPF_API int vpf_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, con
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)tiles), block(NTHREADS);
     const int kern = gemm_kernel_for(epilogue);
-    const int group = tile_group_for(N);
+    const int group = tile_group_for(N, epilogue);
     const int m = (int)M, n = (int)N, k = (int)K;
     switch (epilogue) {
         case VPF_EPI_BIAS: VPF_GEMM_LAUNCH(VPF_EPI_BIAS); break;
