@@ -1,15 +1,22 @@
 #!/bin/bash
-# Build A/B variants of libvpf.so into ab_libs/ (travels to the GPU box; git-ignored): attention chunks-per-barrier.
-# usage: bash tools/ab_libs.sh cpb2 cpb3 ...   then  VPF_LIB_PATH=ab_libs/libvpf_cpb3.so python bench.py ...
+# Build A/B variants of libvpf.so into ab_libs/ (travels to the GPU box; git-ignored): attention chunks-per-barrier
+# (cpbN) or the crop's LDS window size in dwords (cropN).
+# usage: bash tools/ab_libs.sh cpb2 crop10240 ...   then  VPF_LIB_PATH=ab_libs/libvpf_cpb2.so python bench.py ...
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p ab_libs build/ab
 C=vitparticlefiltertracker_amd/csrc
-OBJS=""
-for s in pf_kernels crop gemm_bf16 gemm_mx8 gemm_f32 layernorm cls_attn; do OBJS="$OBJS build/obj/$s.o"; done
+F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -fvisibility=hidden"
 for v in "$@"; do
-  n=${v#cpb}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -fvisibility=hidden \
-      -DVPF_ATTN_CPB=$n -c $C/attention.hip -o build/ab/attention_$v.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab_libs/libvpf_$v.so $OBJS build/ab/attention_$v.o
+  case $v in
+    cpb*) src=attention; def="-DVPF_ATTN_CPB=${v#cpb}" ;;
+    crop*) src=crop; def="-DVPF_CROP_LDS_DW=${v#crop}" ;;
+    *) echo "unknown variant $v"; exit 1 ;;
+  esac
+  OBJS=""
+  for s in pf_kernels crop gemm_bf16 gemm_mx8 gemm_f32 layernorm attention cls_attn; do
+    [ $s = $src ] || OBJS="$OBJS build/obj/$s.o"
+  done
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 $F $def -c $C/$src.hip -o build/ab/${src}_$v.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab_libs/libvpf_$v.so $OBJS build/ab/${src}_$v.o
 done

@@ -168,7 +168,11 @@ __global__ __launch_bounds__(256) void k_crop_patches_fast(const uint32_t* __res
 // into LDS once, and the taps read LDS instead of issuing 32 gathered dword loads per thread through the vector
 // memory path, which bound the global form (the im2col stores are the same). A window larger than CROP_LDS_DW dwords
 // (a large template at a large scale) takes the global taps. Same values and arithmetic as k_crop_patches_fast.
-constexpr int CROP_LDS_DW = 20480;   // 80 KiB: two workgroups per CU; a 64 x 64 template at scale 2 needs 130 x 130
+#ifndef VPF_CROP_LDS_DW
+#define VPF_CROP_LDS_DW 10240   // -DVPF_CROP_LDS_DW=n builds A/B variants (tools/ab_libs.sh)
+#endif
+constexpr int CROP_LDS_DW = VPF_CROP_LDS_DW;   // 40 KiB: four workgroups per CU (0.45-0.49 vs 0.53 ms at 80 KiB and two per CU,
+// profiles/r2_gemm_lab/crop_lds_window_ab.txt); windows up to ~101 x 101 (a 64 x 64 template to scale ~1.55)
 template <typename OutT>
 __global__ __launch_bounds__(512) void k_crop_patches_lds(const uint32_t* __restrict__ rgba, int H, int W,
                                                           const float* __restrict__ xs, const float* __restrict__ ys,
