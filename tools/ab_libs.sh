@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build A/B variants of libvpf.so into ab_libs/ (travels to the GPU box; git-ignored): attention chunks-per-barrier
-# (cpbN) or the crop's LDS window size in dwords (cropN).
+# (cpbN), the crop's LDS window size in dwords (cropN) or the GEMM's MFMAs per A-refill issue (ilvN).
 # usage: bash tools/ab_libs.sh cpb2 crop10240 ...   then  VPF_LIB_PATH=ab_libs/libvpf_cpb2.so python bench.py ...
 set -e
 cd "$(dirname "$0")/.."
@@ -11,6 +11,7 @@ for v in "$@"; do
   case $v in
     cpb*) src=attention; def="-DVPF_ATTN_CPB=${v#cpb}" ;;
     crop*) src=crop; def="-DVPF_CROP_LDS_DW=${v#crop}" ;;
+    ilv*) src=gemm_bf16; def="-DVPF_ILV_SPACING=${v#ilv}" ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
   OBJS=""

@@ -33,6 +33,9 @@ using namespace vpf::gemm;
 namespace {
 
 constexpr int BK = 64;
+#ifndef VPF_ILV_SPACING
+#define VPF_ILV_SPACING 16   // MFMAs per A(t+2) DMA issue in the product loop; -D builds A/B variants (tools/ab_libs.sh)
+#endif
 constexpr int OPERAND_BYTES = BM * BK * 2;      // 32 KiB per operand tile
 static_assert(OPERAND_BYTES == TILE_BYTES, "bf16 K-tile geometry");
 constexpr int STAGE_BYTES = 2 * OPERAND_BYTES;  // A + B
@@ -270,10 +273,11 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads
             __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);    // B(t+1)'s DMA
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {                          // 16 MFMAs per A(t+2) DMA issue
-                __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+            for (int q = 0; q < 4; ++q) {                          // VPF_ILV_SPACING MFMAs per A(t+2) DMA issue
+                __builtin_amdgcn_sched_group_barrier(0x008, VPF_ILV_SPACING, 0);
                 __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
             }
+            if constexpr (VPF_ILV_SPACING < 16) __builtin_amdgcn_sched_group_barrier(0x008, 64 - 4 * VPF_ILV_SPACING, 0);
         } else {
             __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads first
             __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);   // then the 64 MFMAs (counted lgkmcnt waits)
