@@ -1179,14 +1179,14 @@ static int tile_group() {   // VPF_GEMM_GROUP overrides the A-panel group size o
 // Default group per shape (profiles/r2_gemm_lab/group_sweep_r2.txt, one process): the N <= 1024 GEMMs (proj / FC2:
 // 3 column tiles, so a group of 4 A panels keeps 12 tiles of one K panel set in flight) are 1-1.5 % faster with 2
 // panels per group (FC2 3.196 vs 3.226 ms, proj 1.070 vs 1.082), QKV / FC1 with 4. The order never changes a bit.
-// FC1 (EPI_LN_GELU; 12 column tiles at ViT-B) takes 16 A panels per group: -0.9 % on FC1 and the frame -0.7 % in a
-// same-box A/B, although its memory-side requests go up (the extra A re-reads hit the Infinity Cache;
-// profiles/r2_gemm_lab/fc1_group16_pmc.txt).
+// FC1 (EPI_LN_GELU; 12 column tiles at ViT-B) takes 8 A panels per group: 16 was -0.9 % on FC1 and -0.7 % on the frame
+// against 4 in a same-box A/B (profiles/r2_gemm_lab/fc1_group16_pmc.txt), and 8 is another 0.3-0.5 % ahead of 16 in
+// two one-process sweeps (group_sweep_r2s5.txt, fc1_pp_group_ab.txt).
 static int tile_group_for(int64_t N, int epilogue) {
     const int g = tile_group();
     if (g_group_set) return g;
     if (N <= 1024) return 2;
-    return epilogue == VPF_EPI_LN_GELU ? 16 : g;
+    return epilogue == VPF_EPI_LN_GELU ? 8 : g;
 }
 
 // GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, refills issued from the MFMA block (product);
