@@ -93,7 +93,8 @@ def parse():
                          "(host-staged; lets several ranks share one GPU to rehearse the multi-rank path)")
     ap.add_argument("--kernel-frames", type=int, default=2, help="eager frames timed per kernel (roofline)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (s); 0 = skip")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity cores)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every core this process may use (affinity, capped by a cgroup quota / OMP_NUM_THREADS)")
     args = ap.parse_args()
     if args.preset is not None:
         given = {a.lstrip("-").split("=")[0].replace("-", "_") for a in sys.argv[1:] if a.startswith("--")}
@@ -103,8 +104,42 @@ def parse():
     return args
 
 
+def host_cpus():
+    """The host's CPU model and the cores this process may use: its affinity set, capped by a cgroup CPU quota
+    and by OMP_NUM_THREADS when the launcher sets one (the GPU box's CPU share: it sets 16 per GPU)."""
+    info = {"affinity": len(os.sched_getaffinity(0)), "cgroup_quota": None, "omp_num_threads": None, "model": None}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                info["cgroup_quota"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        info["omp_num_threads"] = int(os.environ["OMP_NUM_THREADS"])
+    use = info["affinity"]
+    if info["cgroup_quota"]:
+        use = min(use, max(1, int(info["cgroup_quota"])))
+    if info["omp_num_threads"]:
+        use = min(use, info["omp_num_threads"])
+    info["threads"] = use
+    return info
+
+
 def cpu_baseline(arch_name: str, P: int, budget_s: float, threads: int):
-    """Oracle CPU path on a bounded sample: crops through the fp32 torch ViT + the C PF ops at P."""
+    """Oracle CPU path (the reference's "CPU path": oracle/, torch fp32 ViT + the C particle-filter ops) on a bounded
+    sample of the same workload: crops of the metric's frame through the fp32 ViT for ~budget_s, then the PF ops at the
+    full P. One frame = P crops + the PF ops, so s/frame = (measured s per crop) x P + PF time: a linear extrapolation in
+    the crop count (the oracle runs crops in independent batches of 8), checked by one separately timed full frame
+    (tools/cpu_frame.py, profiles/r3_cpu_full_frame.log)."""
     import numpy as np
     import torch
 
@@ -115,6 +150,8 @@ def cpu_baseline(arch_name: str, P: int, budget_s: float, threads: int):
     from vitparticlefiltertracker_amd.weights import make_vit_weights
 
     arch = ARCHS[arch_name]
+    cpus = host_cpus()
+    threads = threads or cpus["threads"]
     torch.set_num_threads(threads)
     w = make_vit_weights(arch, seed=0)
     frame = synthetic_clip(2)[1]
@@ -143,6 +180,10 @@ def cpu_baseline(arch_name: str, P: int, budget_s: float, threads: int):
     t_pf = time.perf_counter() - t1
     s_per_frame = t_vit * P + t_pf
     return {"value": 1.0 / s_per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
+            "cpu_model": cpus["model"], "host_cpus": {k: cpus[k] for k in ("affinity", "cgroup_quota", "omp_num_threads")},
+            "s_per_frame": round(s_per_frame, 2), "s_per_crop": round(t_vit, 5), "pf_ops_s": round(t_pf, 5),
+            "extrapolation": f"s/frame = s/crop x {P} crops + PF ops at P={P} (linear in crops: independent batches "
+                             f"of {batch}; one full frame timed separately: profiles/r3_cpu_full_frame.log)",
             "sample": f"{crops} crops of {arch_name} fp32 (torch CPU oracle, batch {batch}) in "
                       f"{t_vit * crops:.1f} s + PF ops at P={P}; extrapolated to one {P}-particle frame "
                       f"({s_per_frame:.1f} s/frame)"}
@@ -232,6 +273,8 @@ def main() -> int:
     # the dominant GEMM's MFMA peak: dense bf16, or dense MX-fp8 for the fp8 path's block-scaled GEMMs
     peak = PEAK_FP8_TFLOPS if args.dtype == "fp8" and dom in ("gemm_qkv", "gemm_fc1", "gemm_fc2") else PEAK_BF16_TFLOPS
     gflop_frame = arch.gflop_per_crop() * args.particles
+    gflop_exec = arch.gflop_per_crop_executed(cls_fused=tr.engine.cls_fused) * args.particles
+    check = multi_rank_check(tr, world, rank, dev, args.dist_backend) if world > 1 else None
     line = {
         "metric": METRIC,
         "value": round(fps, 4),
@@ -250,29 +293,72 @@ def main() -> int:
                                "full tracking step per frame",
                    "particles": args.particles, "particles_per_gpu": n_loc, "arch": args.arch, "frame": [fh, fw],
                    "hip_graph": not args.no_graph, "parallelism": f"particle-shard x{world}",
-                   **({"dist_backend": "gloo (ranks share a GPU: rehearsal, not a product number)"}
+                   **({"dist_backend": dist.get_backend(), "dist_world_size": dist.get_world_size()}
+                      if world > 1 else {}),
+                   **({"dist_note": "gloo: ranks may share a GPU (rehearsal, not a product number)"}
                       if world > 1 and args.dist_backend == "gloo" else {})},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "avg_launch_ms": round(ks[dom]["avg_ms"], 4),
                      "flop_per_launch": flops[dom]},
+        # full-forward FLOPs (SURVEY §8d's count, what the metric's roofline is quoted on) and the FLOPs of the work
+        # the product actually performs (the last block computes the CLS row only; config.gflop_per_crop_executed)
         "frame_mfma_frac": round(gflop_frame * 1e9 * fps / (PEAK_BF16_TFLOPS * 1e12 * world), 4),
+        "frame_mfma_frac_executed": round(gflop_exec * 1e9 * fps / (PEAK_BF16_TFLOPS * 1e12 * world), 4),
+        "gflop_per_crop": {"full_forward": round(arch.gflop_per_crop(), 4),
+                           "executed": round(gflop_exec / args.particles, 4)},
         "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                     for k, v in ks.items()},
+        **({"multi_rank_check": check} if check is not None else {}),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         try:
-            line["cpu_baseline"] = cpu_baseline(args.arch, args.particles, args.cpu_seconds, threads)
+            line["cpu_baseline"] = cpu_baseline(args.arch, args.particles, args.cpu_seconds, args.cpu_threads)
         except Exception as e:  # report, never fake
             line["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if check is not None and not check["ok"]:
+        print(f"bench.py: the ranks disagree: {json.dumps(check)}", file=sys.stderr, flush=True)
+        return 1
     return 0
+
+
+def multi_rank_check(tr, world: int, rank: int, dev, backend: str):
+    """N > 1 self-check of the last timed frame (the driver's scaling run proves itself): the backend and world size
+    the process group reports; every rank's estimate bits; a checksum of the global CDF every rank computed from the
+    all-gathered weights (identical iff every rank saw the same global weights); each rank's ancestor range, which
+    must tile the global systematic resample in rank order (ancestors are non-decreasing in the slot index)."""
+    import struct
+
+    import torch
+    import torch.distributed as dist
+    pf = tr.pf
+    est = pf._read_estimate()
+    cdf = pf._cdf.to(torch.int64)
+    mix = torch.arange(1, 2 * cdf.numel(), 2, device=cdf.device, dtype=torch.int64)
+    cdf_sum = int((cdf * mix).sum().item())              # wraps mod 2^64: a checksum, not a value
+    anc = pf.last_ancestors
+    mine = [float(v) for v in est] + [cdf_sum, int(cdf[-1].item()), int(anc[0].item()), int(anc[-1].item()),
+                                      int((anc[1:] >= anc[:-1]).all().item()), int(anc.numel())]
+    t = torch.tensor([struct.unpack("<q", struct.pack("<d", v))[0] if i < 3 else v for i, v in enumerate(mine)],
+                     dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+    out = torch.empty(world * t.numel(), dtype=torch.int64, device=t.device)
+    dist.all_gather_into_tensor(out, t)
+    rows = out.view(world, -1).cpu().tolist()
+    est_bits = [tuple(r[:3]) for r in rows]
+    ok_est = all(e == est_bits[0] for e in est_bits)
+    ok_cdf = all(r[3] == rows[0][3] and r[4] == rows[0][4] for r in rows)
+    ok_anc = all(r[7] == 1 for r in rows) and all(rows[i][6] <= rows[i + 1][5] for i in range(world - 1))
+    ok_cnt = sum(r[8] for r in rows) == pf.P
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "estimates_agree": ok_est,
+            "cdf_checksum_agree": ok_cdf, "ancestors_sorted_across_ranks": ok_anc, "slots_cover_P": ok_cnt,
+            "estimate": [struct.unpack("<d", struct.pack("<q", v))[0] for v in est_bits[0]],
+            "ok": ok_est and ok_cdf and ok_anc and ok_cnt}
 
 
 if __name__ == "__main__":

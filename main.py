@@ -35,8 +35,10 @@ def main(argv=None) -> int:
 
     cfg = load_config(args.config)
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        dist.init_process_group("nccl")
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
+        # device_id binds the RCCL communicator to this rank's GPU eagerly (as bench.py does)
+        dist.init_process_group("nccl", device_id=dev)
     inp = cfg["input"]
     n = args.frames or int(inp["frames"])
     if inp["source"] == "synthetic":

@@ -38,6 +38,11 @@ def test_arch_flops():
     assert abs(C.ARCHS["vit_tiny_patch16_224"].gflop_per_crop() - 2.507) < 0.01
     assert abs(C.ARCHS["vit_large_patch14_336"].gflop_per_crop() - 381.918) < 0.05
     assert C.ARCHS["vit_large_patch14_336"].patch_kp == 640
+    # executed work (the CLS-pruned last block): ViT-B loses one block's 2.908 GFLOP, keeps 0.021 of it
+    b = C.ARCHS["vit_base_patch16_224"]
+    assert abs(b.gflop_per_crop_executed(True) - 32.2396) < 1e-3
+    assert b.gflop_per_crop_executed(False) > b.gflop_per_crop_executed(True)
+    assert b.gflop_per_crop() - b.gflop_per_crop_executed(False) > 2.0
 
 
 def test_host_philox_matches_oracle():
@@ -161,3 +166,31 @@ def test_c_abi_rejects_bad_shapes_before_any_launch():
     assert sk(fake, 768, fake, fake, None, None, None, fake, 768, 4, 768, 768, 0, 5, None, fake, 10 ** 7, None) == -1
     assert sk(fake, 768, fake, fake, None, None, None, fake, 768, 4, 768, 768, 0, 3, None, fake, 100, None) == -1
     assert sk(fake, 768, fake, fake, None, None, None, fake, 768, 4, 768, 768, 4, 3, None, fake, 10 ** 7, None) == -1
+
+
+def test_checkpoint_paths_round_trip():
+    """the per-rank file save_checkpoint returns is accepted by load_checkpoint as is (no second suffix),
+    and so is the base path, for one rank and for several."""
+    from vitparticlefiltertracker_amd.tracker import Tracker
+    t = Tracker.__new__(Tracker)              # host logic only: no device state needed
+    for rank, world, base, want in ((0, 1, "ck", "ck.npz"), (0, 1, "ck.npz", "ck.npz"),
+                                    (2, 4, "ck", "ck.rank2of4.npz"), (2, 4, "ck.rank2of4.npz", "ck.rank2of4.npz")):
+        t.rank, t.world_size = rank, world
+        f = t._checkpoint_file(base)
+        assert f == want and t._checkpoint_file(f) == f
+
+
+def test_gemm_tune_rejects_lab_only_kernels():
+    """the timing probes that never write C (kernels 8 / 9) are not in the product library, so a stray
+    vpf_gemm_tune call cannot turn every GEMM into garbage; real variants are still accepted (host state only)."""
+    from vitparticlefiltertracker_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    L = _lib.lib()
+    try:
+        assert L.vpf_gemm_tune(8, -1) == -1 and L.vpf_gemm_tune(9, -1) == -1
+        assert L.vpf_gemm_tune(17, -1) == -1 and L.vpf_gemm_tune(-2, -1) == -1
+        for k in (1, 5, 7, 10, 13, 16):
+            assert L.vpf_gemm_tune(k, -1) == 0
+    finally:
+        assert L.vpf_gemm_tune(0, -1) == 0

@@ -93,6 +93,51 @@ def test_crop_identity_kat():
     assert np.array_equal(out, ref)
 
 
+@pytest.mark.parametrize("H,W,S,patch,box", [(150, 210, 32, 8, (48.0, 40.0)), (224, 224, 224, 16, (64.0, 64.0)),
+                                              (96, 72, 28, 14, (30.0, 52.0))])
+def test_crop_matches_grid_sample(H, W, S, patch, box):
+    """the crop restatement (SPEC S3) against torch.nn.functional.grid_sample, the semantics SPEC S3
+    names (README.md:7 "feature extraction" of the particle's box): bilinear, align_corners=False, zero padding on
+    the raw 0..255 frame, then the per-channel normalisation. Non-unit scales, boxes partly and wholly off the
+    frame, non-square frames and boxes, non-trivial mean / std. The sample positions are SPEC S3's fp32 arithmetic
+    (the oracle's own), handed to grid_sample as float64 normalised coordinates, so the check isolates the
+    sampling and the padding rule: fp32 oracle vs float64 grid_sample within 1e-5."""
+    import torch
+    import torch.nn.functional as Fn
+    rng = np.random.default_rng(H + W + S)
+    frame = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    cases = [(W * 0.47 + 0.3, H * 0.47 + 0.7, 0.63), (12.0, 9.5, 1.9), (W - 5.0, H - 3.0, 1.3),
+             (-20.0, H * 0.4, 0.8), (W * 0.5, H * 0.5, 3.7), (W + 200.0, -50.0, 1.0), (W * 0.3, H * 0.6, 0.5017)]
+    part = np.ascontiguousarray(np.array(cases, np.float32).T)
+    n = part.shape[1]
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    kp = -(-3 * patch * patch // 64) * 64
+    out = pf.crop_patches(frame, part, box, S, patch, kp, mean, std)
+    f32 = np.float32
+    grid = np.empty((n, S, S, 2), np.float64)
+    o = np.arange(S, dtype=np.float32)
+    for p in range(n):
+        x, y, s = part[:, p]
+        bw, bh = f32(s * f32(box[0])), f32(s * f32(box[1]))
+        x0, y0 = f32(x - f32(0.5) * bw), f32(y - f32(0.5) * bh)
+        dx, dy = f32(bw / f32(S)), f32(bh / f32(S))
+        sx = ((x0 + (o + f32(0.5)) * dx).astype(np.float32) - f32(0.5)).astype(np.float32)   # SPEC S3, fp32
+        sy = ((y0 + (o + f32(0.5)) * dy).astype(np.float32) - f32(0.5)).astype(np.float32)
+        grid[p, :, :, 0] = (2.0 * sx.astype(np.float64)[None, :] + 1.0) / W - 1.0            # align_corners=False
+        grid[p, :, :, 1] = (2.0 * sy.astype(np.float64)[:, None] + 1.0) / H - 1.0
+    img = torch.from_numpy(frame.astype(np.float64)).permute(2, 0, 1).unsqueeze(0).expand(n, 3, H, W)
+    crop = Fn.grid_sample(img, torch.from_numpy(grid), mode="bilinear", padding_mode="zeros", align_corners=False)
+    a, b = pf.norm_affine(mean, std)
+    norm = crop * torch.from_numpy(a.astype(np.float64)).view(1, 3, 1, 1) + torch.from_numpy(b.astype(np.float64)).view(1, 3, 1, 1)
+    g = S // patch
+    ref = norm.reshape(n, 3, g, patch, g, patch).permute(0, 2, 4, 1, 3, 5).reshape(n * g * g, 3 * patch * patch)
+    np.testing.assert_allclose(out[:, :3 * patch * patch].astype(np.float64), ref.numpy(), rtol=0, atol=1e-5)
+    assert np.all(out[:, 3 * patch * patch:] == 0)
+    # the off-frame box is pure padding: every sample is the normalised zero (b_c)
+    off = out[5 * g * g:6 * g * g, :3 * patch * patch].reshape(g * g, 3, patch * patch)
+    assert np.array_equal(off, np.broadcast_to(b.reshape(1, 3, 1), off.shape))
+
+
 def test_crop_zero_padding_and_kp_pad():
     frame = np.full((50, 60, 3), 200, np.uint8)
     part = np.array([[-500.0], [-500.0], [1.0]], np.float32)      # box entirely outside the frame

@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU session: each GPU step under its own time limit; stop at the first crash / timeout / abort.
-# Usage: tools/gpu_session.sh <tag> [tests] [smoke] [bench] [bench_np] [prof] [lab]
+# Usage: tools/gpu_session.sh <tag> [host] [tests] [scale] [smoke] [bench] [bench_l] [bench8] [prof] [pmc] [pmc8]
+#        [pfprobe] [cpuframe] [lab]
 #   env: PYTEST_K (pytest -k filter for "tests"), LAB_SHAPES / LAB_VARS (gemm_lab filters)
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -15,8 +16,21 @@ rocm-smi --showproductname > $OUT/gpu.txt 2>&1 || true
 for step in "$@"; do
   case $step in
     tests)
-      timeout -k 10 1500 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 -rf ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 900 --timeout-method thread -rf ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1
       ok_or_stop $? tests; tail -30 $OUT/pytest_gpu.log ;;
+    host)   # the box's CPU share (bench.py cpu_baseline's core count) and model
+      { echo "nproc=$(nproc) affinity=$(python3 -c 'import os;print(len(os.sched_getaffinity(0)))') OMP_NUM_THREADS=$OMP_NUM_THREADS";
+        cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -m1 "model name" /proc/cpuinfo; free -g | head -2; } > $OUT/host.txt 2>&1
+      cat $OUT/host.txt ;;
+    scale)  # the benchmark-size parity tests alone (tests/test_gpu_scale.py)
+      timeout -k 10 1100 python -u -m pytest tests/test_gpu_scale.py -m gpu -v -p no:cacheprovider --timeout 900 --timeout-method thread -rf > $OUT/pytest_scale.log 2>&1
+      ok_or_stop $? scale; tail -15 $OUT/pytest_scale.log ;;
+    pfprobe)
+      timeout -k 10 300 python tools/pf_probe.py > $OUT/pf_probe.log 2>&1
+      ok_or_stop $? pfprobe; cat $OUT/pf_probe.log | grep particles ;;
+    cpuframe)
+      timeout -k 10 900 python tools/cpu_frame.py > $OUT/cpu_frame.log 2> $OUT/cpu_frame.err
+      ok_or_stop $? cpuframe; tail -2 $OUT/cpu_frame.err; cut -c1-600 $OUT/cpu_frame.log ;;
     smoke)
       timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
       ok_or_stop $? smoke; tail -5 $OUT/smoke.log ;;

@@ -59,6 +59,22 @@ class ViTArch:
         f = 2 * (n * self.patch_k * D + L * (N * D * 3 * D + 2 * H * N * N * hd + N * D * D + 2 * N * D * F))
         return f / 1e9
 
+    def gflop_per_crop_executed(self, cls_fused: bool = True) -> float:
+        """FLOPs of the work the product path performs per crop, in GFLOP: the full forward of blocks 0..L-2, and for
+        the last block only what its CLS row needs (vit.py ViTEngine.encoder: the final LayerNorm reads nothing else).
+        cls_fused (csrc/cls_attn.hip): the CLS query (2 D^2), G = W'_k^T q per head (2 D^2 useful), the folded
+        attention's scores and weighted row sum over N tokens (4 N D H), W'_v per head (2 D^2 useful), proj (2 D^2),
+        fc1 / fc2 (4 D F). Otherwise K and V for every row (4 N D^2), the CLS query, its attention (4 H N hd) and
+        the CLS row's proj / MLP. The block-diagonal GEMMs' discarded products are not counted."""
+        n, N, D, L, H, hd, F = self.n_patches, self.tokens, self.dim, self.depth, self.heads, self.head_dim, self.mlp
+        full_block = N * D * 3 * D + 2 * H * N * N * hd + N * D * D + 2 * N * D * F
+        if cls_fused:
+            last = D * D + D * D + 2 * N * D * H + D * D + D * D + 2 * D * F
+        else:
+            last = 2 * N * D * D + D * D + 2 * H * N * hd + D * D + 2 * D * F
+        f = 2 * (n * self.patch_k * D + (L - 1) * full_block + last)
+        return f / 1e9
+
 
 ARCHS: Dict[str, ViTArch] = {
     "vit_tiny_patch16_224": ViTArch("vit_tiny_patch16_224", 224, 16, 192, 12, 3, 768),

@@ -1091,6 +1091,29 @@ void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__
 // fp8 copies are produced by the residual-stream producers only (proj, patch embed): the only bf16 GEMMs
 // whose output an MX8 GEMM reads
 #define VPF_GEMM_PT_OK(E) ((E) == VPF_EPI_LN || (E) == VPF_EPI_LN_GELU || (E) == VPF_EPI_BIAS || (E) == VPF_EPI_BIAS_GELU)
+// Kernels 8 / 9 (LAB 1 / 2: the C stores predicated off / no epilogue at all) never write their output: timing-only
+// variants, compiled into lab builds alone (-DVPF_GEMM_LAB, tools/gemm_lab). A product build rejects them in
+// vpf_gemm_tune and ignores them in VPF_GEMM_KERNEL.
+#ifdef VPF_GEMM_LAB
+constexpr bool kGemmLab = true;
+#define VPF_GEMM_LAB_LAUNCH(E)                                                                               \
+    else if ((kern == 8 || kern == 9) && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {    \
+        if (kern == 8)                                                                                       \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 1>), grid, block, 0, s,   \
+                               A, (int)lda, W, bias, residual, pos, patch_rows,                               \
+                               reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,        \
+                               group | 0x10000, stats_parts, ln_eps, stats_out, stats_rows, o8);              \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 2>), grid, block, 0, s,   \
+                               A, (int)lda, W, bias, residual, pos, patch_rows,                               \
+                               reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,        \
+                               group | 0x10000, stats_parts, ln_eps, stats_out, stats_rows, o8);              \
+    }
+#else
+constexpr bool kGemmLab = false;
+#define VPF_GEMM_LAB_LAUNCH(E)
+#endif
+static bool gemm_kernel_ok(int k) { return k >= 1 && k <= 16 && (kGemmLab || (k != 8 && k != 9)); }
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
         if constexpr (VPF_GEMM_PT_OK(E)) {                                                                   \
@@ -1114,24 +1137,15 @@ void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__
         if (kern == 16 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                  \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 4>), grid, block, 0, s,   \
                                VPF_GEMM_ARGS);                                                               \
-        } else if (kern >= 8 && kern <= 12 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) { \
-            if (kern >= 10)                                                                                  \
-                hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 3>), grid, block, 0, s, \
-                                   A, (int)lda, W, bias, residual, pos, patch_rows,                           \
-                                   reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,    \
-                                   group | ((kern == 10 ? 2 : kern == 11 ? 1 : 3) << 17), stats_parts, ln_eps, \
-                                   stats_out, stats_rows, o8);                                                \
-            else if (kern == 8)                                                                              \
-                hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 1>), grid, block, 0, s, \
-                                   A, (int)lda, W, bias, residual, pos, patch_rows,                           \
-                                   reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,    \
-                                   group | 0x10000, stats_parts, ln_eps, stats_out, stats_rows, o8);          \
-            else                                                                                             \
-                hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 2>), grid, block, 0, s, \
-                                   A, (int)lda, W, bias, residual, pos, patch_rows,                           \
-                                   reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,    \
-                                   group | 0x10000, stats_parts, ln_eps, stats_out, stats_rows, o8);          \
-        } else if (kern == 2)                                                                                \
+        } else if (kern >= 10 && kern <= 12 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) { \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 3>), grid, block, 0, s,   \
+                               A, (int)lda, W, bias, residual, pos, patch_rows,                               \
+                               reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,        \
+                               group | ((kern == 10 ? 2 : kern == 11 ? 1 : 3) << 17), stats_parts, ln_eps,     \
+                               stats_out, stats_rows, o8);                                                    \
+        }                                                                                                    \
+        VPF_GEMM_LAB_LAUNCH(E)                                                                               \
+        else if (kern == 2)                                                                                  \
             hipLaunchKernelGGL((k_gemm_bf16<E, false>), grid, block, 0, s, VPF_GEMM_ARGS);                    \
         else if (kern == 3 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
             hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, false>), grid, block, 0, s, VPF_GEMM_ARGS); \
@@ -1192,7 +1206,8 @@ static int tile_group_for(int64_t N, int epilogue) {
 // GEMM kernel selection: 1 = k_gemm_bf16 with the deep A ring, refills issued from the MFMA block (product);
 // 2 = the 2-stage ring, 3 = the deep ring with both refills issued right after the barrier, 4 = kernel 1 with the
 // two-pass epilogue, 5 = the ping-pong loop k_gemm_pp, 6 = kernel 1 with the original epilogue row order, 7 = the
-// four-wave k_gemm_w4, 8 / 9 = kernel 1 without its C stores / without its epilogue (A/B timing; outputs not written), 10 / 11 / 12 = kernel 1
+// four-wave k_gemm_w4, 8 / 9 = kernel 1 without its C stores / without its epilogue (A/B timing; outputs not written;
+// -DVPF_GEMM_LAB builds only), 10 / 11 / 12 = kernel 1
 // with a staggered start in 4 / 2 / 8 phases, 13 = the persistent k_gemm_pt (LN / LN_GELU / BIAS / BIAS_GELU; else 1).
 // VPF_GEMM_KERNEL sets the initial value, vpf_gemm_tune() the current one.
 static int g_kernel = -1;
@@ -1202,7 +1217,7 @@ static int gemm_kernel() {
         const char* e = getenv("VPF_GEMM_KERNEL");
         g_kernel = e ? atoi(e) : 1;
         g_kernel_set = e != nullptr;
-        if (g_kernel < 1 || g_kernel > 16) g_kernel = 1;
+        if (!gemm_kernel_ok(g_kernel)) { g_kernel = 1; g_kernel_set = false; }
     }
     return g_kernel;
 }
@@ -1221,7 +1236,7 @@ int vpf_gemm_tile_group_mx8(int epilogue) {
     return g_group_set ? g : (epilogue == VPF_EPI_LN ? 8 : g);
 }
 VPF_API int vpf_gemm_tune(int kernel, int group) {
-    if (kernel < 0 || kernel > 16) return VPF_ERR_ARG;
+    if (kernel != 0 && !gemm_kernel_ok(kernel)) return VPF_ERR_ARG;
     gemm_kernel();
     tile_group();
     if (kernel == 0) {   // back to the per-shape defaults (kernel and group)

@@ -187,28 +187,43 @@ class Tracker:
         self.template.copy_(t / t.norm())
 
     # ------------------------------------------------------------------ checkpoint / resume
+    def config_fingerprint(self) -> dict:
+        """Every configuration value a tracking frame's arithmetic depends on: a checkpoint records
+        these and a resume under any other value is refused instead of drifting from the original run."""
+        c = self.cfg
+        m, p, lk = c["model"], c["particles"], c["likelihood"]
+        return {"arch": self.arch.name, "dtype": str(m["dtype"]), "weights_seed": int(m["weights"]["seed"]),
+                "mean": [float(v) for v in m["mean"]], "std": [float(v) for v in m["std"]],
+                "P": int(p["num"]), "motion_std": [float(v) for v in p["motion_std"]],
+                "scale_range": [float(v) for v in p["scale_range"]], "seed": int(p["seed"]),
+                "lambda": float(lk["lambda"]), "weight_bits": int(lk["weight_bits"]),
+                "template_update": float(lk["template_update"]), "rank": self.rank, "world_size": self.world_size}
+
     def state_dict(self) -> dict:
         """The tracker's state between frames as numpy arrays: this rank's particles (after the last resample, so
-        Q is zero), the template, the template box, the frame size and the frame index. The motion noise and the
-        resample word are counter-based (seed, frame index, global particle index: SPEC S1/S2), so a tracker that
-        loads this continues bit for bit."""
+        Q is zero), the template, the template box, the frame size and the frame index, plus the configuration
+        fingerprint (JSON). The motion noise and the resample word are counter-based (seed, frame index, global
+        particle index: SPEC S1/S2), so a tracker with the same configuration that loads this continues bit for
+        bit."""
+        import json
         if self.pf is None:
             raise RuntimeError("call init(frame, bbox) first")
-        return {"format": np.int64(1), "frame_index": np.int64(self.frame_index),
+        return {"format": np.int64(2), "frame_index": np.int64(self.frame_index),
                 "pf_frame": np.int64(self.pf.frame), "particles": self.pf.particles.cpu().numpy(),
                 "template": self.template.cpu().numpy(), "box_wh": np.array(self.box_wh, np.float64),
                 "frame_hw": np.array([self.pf.height, self.pf.width], np.int64),
-                "P": np.int64(self.pf.P), "rank": np.int64(self.rank), "world_size": np.int64(self.world_size),
-                "seed": np.int64(self.pf.seed), "arch": np.array(self.arch.name)}
+                "config": np.array(json.dumps(self.config_fingerprint(), sort_keys=True))}
 
     def load_state_dict(self, sd: dict) -> None:
-        if int(sd["format"]) != 1:
+        import json
+        if int(sd["format"]) != 2:
             raise ValueError("unknown checkpoint format")
         c = self.cfg
-        if (int(sd["P"]) != int(c["particles"]["num"]) or int(sd["rank"]) != self.rank
-                or int(sd["world_size"]) != self.world_size or str(sd["arch"]) != self.arch.name
-                or int(sd["seed"]) != int(c["particles"]["seed"])):
-            raise ValueError("checkpoint was written by a tracker with another configuration or rank layout")
+        saved, mine = json.loads(str(sd["config"])), self.config_fingerprint()
+        diff = sorted(k for k in set(saved) | set(mine) if saved.get(k) != mine.get(k))
+        if diff:
+            raise ValueError("checkpoint was written by a tracker with another configuration or rank layout: "
+                             + ", ".join(f"{k} {saved.get(k)!r} != {mine.get(k)!r}" for k in diff))
         H, W = (int(v) for v in sd["frame_hw"])
         self.box_wh = tuple(float(v) for v in sd["box_wh"])
         t = torch.from_numpy(np.ascontiguousarray(sd["template"], dtype=np.float32)).to(self.device)
@@ -227,21 +242,21 @@ class Tracker:
         self.frame_index = int(sd["frame_index"])
         self._graph = None
 
+    def _checkpoint_file(self, path: str) -> str:
+        """`<path>.rank<r>of<G>.npz` with several ranks, `<path>.npz` with one; a path that already names this
+        rank's file (what save_checkpoint returned) is taken as is, so save -> load round-trips either way."""
+        suffix = f".rank{self.rank}of{self.world_size}.npz" if self.world_size > 1 else ".npz"
+        return path if path.endswith(suffix) else path + suffix
+
     def save_checkpoint(self, path: str) -> str:
         """np.savez of state_dict() (no pickled objects); with several ranks each writes `<path>.rank<r>of<G>.npz`.
-        Returns the file written."""
-        if self.world_size > 1:
-            path = f"{path}.rank{self.rank}of{self.world_size}.npz"
-        elif not path.endswith(".npz"):
-            path = path + ".npz"
+        Returns the file written (load_checkpoint accepts it, or the base path)."""
+        path = self._checkpoint_file(path)
         np.savez(path, **self.state_dict())
         return path
 
     def load_checkpoint(self, path: str) -> None:
-        if self.world_size > 1:
-            path = f"{path}.rank{self.rank}of{self.world_size}.npz"
-        elif not path.endswith(".npz"):
-            path = path + ".npz"
+        path = self._checkpoint_file(path)
         with np.load(path, allow_pickle=False) as z:
             self.load_state_dict({k: z[k] for k in z.files})
 
