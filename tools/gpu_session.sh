@@ -25,6 +25,9 @@ for step in "$@"; do
     scale)  # the benchmark-size parity tests alone (tests/test_gpu_scale.py)
       timeout -k 10 1100 python -u -m pytest tests/test_gpu_scale.py -m gpu -v -p no:cacheprovider --timeout 900 --timeout-method thread -rf > $OUT/pytest_scale.log 2>&1
       ok_or_stop $? scale; tail -15 $OUT/pytest_scale.log ;;
+    attnab)
+      timeout -k 10 300 python tools/attn_ab.py $ATTN_VARIANTS > $OUT/attn_ab.log 2>&1
+      ok_or_stop $? attnab; cat $OUT/attn_ab.log | grep -v amdgpu.ids ;;
     pfprobe)
       timeout -k 10 300 python tools/pf_probe.py > $OUT/pf_probe.log 2>&1
       ok_or_stop $? pfprobe; cat $OUT/pf_probe.log | grep particles ;;

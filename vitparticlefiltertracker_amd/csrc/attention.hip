@@ -16,6 +16,7 @@
 // fp32 parity path (vpf_attention_f32): one thread per query, K/V of the head in LDS as fp32, exact
 // expf softmax (N <= 256).
 #include <cstdlib>
+#include <type_traits>
 
 #include "vpf_common.h"
 #include "mx8.h"
@@ -253,6 +254,99 @@ __device__ __forceinline__ void attn_step_tail8(const char* Ks, const char* Vs, 
     }
 }
 
+// 16-query strip on v_mfma_f32_16x16x32_bf16: the last strip when it holds at most 16 real queries (N = 197 ->
+// queries 192..207, 5 real), at half the MFMA and softmax work of a 32-query strip (which spent 27 of its 32 rows
+// on padding). Operand maps of 16x16x32 (g = lane / 16): A lane = row lane % 16, K slots 8g .. 8g+7; B lane = column
+// lane % 16, the same K slots; D lane = rows 4g .. 4g+3 of column lane % 16.
+//   S^T = K Q^T per 16-key tile kt: A = K rows kb + 16 kt + lane % 16 (dims 32 kk + 8g ..), B = Q^T (query
+//   q0 + lane % 16, dims 32 kk + 8g ..), so lane (query lane % 16, g) holds the scores of keys kb + 16 kt + 4g + r.
+//   A query's row max / sum combine the 4 lanes lane % 16 + 16g (permlane16 + permlane32 swaps).
+//   O^T += V^T P^T with the PV K slots permuted: slot 8g + 4 kt + r <-> key kb + 16 kt + 4g + r. The lane's own
+//   8 probabilities are then its B fragment as they stand, and its V^T A fragment is two transposed reads: lane
+//   16g + 4q + p supplies row kb + 4g + q (then + 16 rows = + 2048 B: the V swizzle keeps bit 1 of the row), dims
+//   16 dt + 4p .. +3, and receives dim 16 dt + lane % 16 of those 4 keys (cdna_hip_programming.md T10).
+//   O^T lane = dims 16 dt + 4g .. +3 of query lane % 16.
+// MASK: keys >= N get probability 0 (the padded K / V rows are finite copies of row N - 1).
+__device__ __forceinline__ float xor16_max(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    float y;   // scores are never NaN: one v_max_f32 (as xor32_max)
+    asm("v_max_f32 %0, %1, %2" : "=v"(y) : "v"(__uint_as_float(r[0])), "v"(__uint_as_float(r[1])));
+    return y;
+}
+__device__ __forceinline__ float xor16_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool MASK>
+__device__ __forceinline__ void attn_step16(const char* Ks, const char* Vs, int kb, int N, int lane, const bf16x8 qf[2],
+                                            float scale_log2, float& m, float& l, f32x4 (&o)[4]) {
+    const int r16 = lane & 15, g = lane >> 4;
+    f32x4 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int kr = kb + 16 * kt + r16;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, 4 * kk + g));
+            s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], s[kt], 0, 0, 0);
+        }
+    }
+    float bm = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if constexpr (MASK) {
+                if (kb + 16 * kt + 4 * g + r >= N) s[kt][r] = -INFINITY;
+            }
+            bm = fmaxf(bm, s[kt][r]);
+        }
+    bm = xor32_max(xor16_max(bm));
+    if (__builtin_expect(__any(bm > m + 8.0f / scale_log2), 0)) {   // lazy rescale, as attn_step
+        const float mn = fmaxf(m, bm);
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
+    }
+    const float msc = m * scale_log2;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, -msc));
+            s[kt][r] = p;
+            l += p;
+        }
+    const uint4 u = make_uint4(pack_bf2(s[0][0], s[0][1]), pack_bf2(s[0][2], s[0][3]), pack_bf2(s[1][0], s[1][1]),
+                               pack_bf2(s[1][2], s[1][3]));
+    const bf16x8 pf = __builtin_bit_cast(bf16x8, u);
+    const int q = r16 >> 2, p4 = r16 & 3;
+    bf16x4 vr[4][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+        const int c16 = 2 * dt + (p4 >> 1), inner = 8 * (p4 & 1);
+        const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(kb + 4 * g + q, c16) + inner);
+        vr[dt][0] = ds_read_tr_asm_o<0>(a);
+        vr[dt][1] = ds_read_tr_asm_o<2048>(a);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0]), "+v"(vr[0][1]), "+v"(vr[1][0]), "+v"(vr[1][1]),
+                 "+v"(vr[2][0]), "+v"(vr[2][1]), "+v"(vr[3][0]), "+v"(vr[3][1])::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+        const bf16x4 lo = vr[dt][0], hi = vr[dt][1];
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+    }
+}
+
 // One workgroup per (particle, head); one wave per 32-query strip (up to 8 waves, strips beyond loop).
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                    int N, int H, float scale_log2, int q_rows) {
@@ -359,7 +453,13 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 constexpr int PIPE_CPB = VPF_ATTN_CPB;
 // OUT8: the output is written as MX8 (the fp8 path's proj A operand) instead of bf16: the same packed bf16
 // values, quantised per 32-dim block (a block = 16 dims of a lane + 16 of its partner half-wave lane).
-template <int CPB, bool OUT8 = false, bool TAIL8 = true>
+// TAIL16: when the last strip holds at most 16 real queries (q_rows % 32 in 1..16: N = 197), its wave runs the
+// 16-query step (attn_step16) instead of a 32-query strip. That wave runs the same chunk loop (run_strip below, one
+// template for both strip kinds), so every wave of the workgroup passes the same barriers at the same chunks: a wave
+// whose loop took another barrier schedule would release its partners' reads of K / V chunks that have not landed
+// (the round-2 attempt at this tail, which gave its 16-query wave a chunk loop of its own, read such chunks: NaNs
+// on the 32-query strips).
+template <int CPB, bool OUT8 = false, bool TAIL8 = true, bool TAIL16 = true>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_pipe(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows,
     uint8_t* __restrict__ out8 = nullptr, int ld8 = 0, uint8_t* __restrict__ s8 = nullptr, int lds8 = 0) {
@@ -377,13 +477,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31, hh = lane >> 5;
     const int nstrips = (q_rows + 31) >> 5;
+    // wave-uniform: this wave's strip holds query N - 1 and at most 16 real queries. Decided by N, not q_rows, so a
+    // row's result does not depend on how many rows the call computes.
+    const int nlast = (N - 1) >> 5;
+    const bool w16 = TAIL16 && !OUT8 && wid == nlast && wid < nstrips && N - 32 * nlast <= 16;
 
     const int q = wid * 32 + l32;
     // Q fragments by inline-asm loads: hipcc does not count them, so it cannot merge them into a vmcnt(0) at
     // the first MFMA (which would also drain every K/V chunk). They are older than all DMA pieces, so the
     // first chunk's counted wait retires them; the empty asm after it pins every use below that wait.
+    // 16-query strip: qf[kk] (kk < 2) = Q[32 wid + lane % 16][32 kk + 8 (lane / 16) ..] (attn_step16's B operand).
     bf16x8 qf[4];
-    {
+    if (w16) {
+        const bf16_t* qp = qbase + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[kk]) : "v"(qp + kk * 32));
+    } else {
         const bf16_t* qp = qbase + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + ks * 16));
@@ -402,29 +511,61 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
     }
     const bool active = wid < nstrips;
-    f32x16 o0 = {}, o1 = {};
-    float m = -INFINITY, l = 0.f;
     const int nfull = N >> 5;             // chunks without padded keys
-    int c = 0;
-    for (; c < nfull; ++c) {
-        if (c % CPB == 0) {   // chunks c .. c+CPB-1 landed for every wave
-            wait_vmcnt(max(NT - c - CPB, 0));
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+    // The chunk loop, one template for both strip kinds: the barrier schedule (a counted wait + s_barrier before
+    // chunks 0, CPB, 2 CPB, ..., and before the padded tail chunk) depends on N and CPB only.
+    auto run_strip = [&](auto k16, f32x16& o0, f32x16& o1, f32x4 (&o16)[4], float& m, float& l) {
+        constexpr bool W16 = decltype(k16)::value;
+        auto pin_q = [&]() {
+            if constexpr (W16) asm volatile("" : "+v"(qf[0]), "+v"(qf[1]) :: "memory");
+            else asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        };
+        int c = 0;
+        for (; c < nfull; ++c) {
+            if (c % CPB == 0) {   // chunks c .. c+CPB-1 landed for every wave
+                wait_vmcnt(max(NT - c - CPB, 0));
+                __builtin_amdgcn_s_barrier();
+                pin_q();
+            }
+            if (active) {
+                if constexpr (W16) attn_step16<false>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
+                else attn_step<1, false, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+            }
         }
-        if (active) attn_step<1, false, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+        if (c < NT) {
+            if (c % CPB == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                pin_q();
+            }
+            if (active) {
+                if constexpr (W16) attn_step16<true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
+                else if (TAIL8 && N - c * 32 <= 8) attn_step_tail8(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                else attn_step<1, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+            }
+        }
+    };
+    float m = -INFINITY, l = 0.f;
+    if (w16) {
+        f32x16 o0 = {}, o1 = {};
+        f32x4 o16[4] = {};
+        run_strip(std::true_type{}, o0, o1, o16, m, l);
+        // the 4 lanes lane % 16 + 16 g share query 32 wid + lane % 16; lane holds dims 16 dt + 4g .. +3
+        l = xor32_sum(xor16_sum(l));
+        const float inv = 1.0f / l;
+        const int qq = wid * 32 + (lane & 15);
+        if (qq < q_rows) {
+            bf16_t* orow = out + (row0 + qq) * D + h * HD + 4 * (lane >> 4);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+                *reinterpret_cast<uint2*>(orow + 16 * dt) = make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
+                                                                      pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
+        }
+        return;
     }
-    if (c < NT) {
-        if (c % CPB == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
-        }
-        if (active) {
-            if (TAIL8 && N - c * 32 <= 8) attn_step_tail8(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-            else attn_step<1, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-        }
-    }
+    f32x16 o0 = {}, o1 = {};
+    f32x4 o16_unused[4];
+    run_strip(std::false_type{}, o0, o1, o16_unused, m, l);
     if (!active) return;
     l = xor32_sum(l);
     const float inv = 1.0f / l;
@@ -664,23 +805,25 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     // whole-image kernel instead (A/B timing); N > 256 always takes it (waves loop over strips).
     const char* mode = getenv("VPF_ATTN_MODE");
     if (N <= 256 && !(mode && mode[0] == '0')) {
-        // VPF_ATTN_TAIL=0: the general masked last step instead of attn_step_tail8 (A/B timing)
+        // VPF_ATTN_TAIL=0: the general masked last step instead of attn_step_tail8; VPF_ATTN_TAIL16=0: the last
+        // strip as a 32-query strip even when it holds <= 16 queries (A/B timing; every variant is tested)
         const char* tail = getenv("VPF_ATTN_TAIL");
-        const bool tail8 = !(tail && tail[0] == '0');
+        const char* t16 = getenv("VPF_ATTN_TAIL16");
+        const bool tail8 = !(tail && tail[0] == '0'), tail16 = !(t16 && t16[0] == '0');
+        typedef void (*pipe_fn)(const bf16_t*, bf16_t*, int, int, float, int, uint8_t*, int, uint8_t*, int);
+        static const pipe_fn fns[4] = {k_attn_bf16_pipe<PIPE_CPB, false, false, false>,
+                                       k_attn_bf16_pipe<PIPE_CPB, false, false, true>,
+                                       k_attn_bf16_pipe<PIPE_CPB, false, true, false>,
+                                       k_attn_bf16_pipe<PIPE_CPB, false, true, true>};
         static bool pipe_attr = false;   // benign race: idempotent attribute set
         if (!pipe_attr) {
-            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, false, true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, false, false>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            for (pipe_fn f : fns)
+                (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             pipe_attr = true;
         }
-        if (tail8)
-            hipLaunchKernelGGL((k_attn_bf16_pipe<PIPE_CPB, false, true>), dim3((unsigned)(B * H)), dim3(512), lds,
-                               (hipStream_t)stream, qkv, out, N, H, scale_log2, q_rows);
-        else
-            hipLaunchKernelGGL((k_attn_bf16_pipe<PIPE_CPB, false, false>), dim3((unsigned)(B * H)), dim3(512), lds,
-                               (hipStream_t)stream, qkv, out, N, H, scale_log2, q_rows);
+        hipLaunchKernelGGL(fns[2 * tail8 + tail16], dim3((unsigned)(B * H)), dim3(512), lds, (hipStream_t)stream, qkv,
+                           reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows, (uint8_t*)nullptr, 0,
+                           (uint8_t*)nullptr, 0);
         VPF_RETURN_LAUNCH();
     }
     const int threads = 64 * (strips < 8 ? strips : 8);
