@@ -269,7 +269,7 @@ def test_gemm_kernel_variants_bit_identical(M, N, K):
         for epi in (0, 1, 2, 4, 5):
             assert L.vpf_gemm_tune(1, -1) == 0
             ref, ref_st = run(epi)
-            for k in (0, 2, 3, 4, 5, 6, 7, 10, 13, 16):   # 0: the per-shape defaults the product runs
+            for k in (0, 2, 3, 4, 5, 6, 7, 10, 13, 16, 17):   # 0: the per-shape defaults the product runs
                 assert L.vpf_gemm_tune(k, -1) == 0
                 got, st = run(epi)
                 assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (k, epi)
@@ -316,6 +316,58 @@ def test_gemm_persistent_bit_identical(M, N, K):
                 assert bad == 0, (k, epi, bad)
     finally:
         L.vpf_gemm_tune(0, -1)                # the per-shape defaults
+
+
+@pytest.mark.parametrize("M,N,K,P", [(806912 // 4, 3072, 768, 12), (806912 // 8, 768, 3072, 12), (3001, 2304, 64, 12),
+                                     (5000, 768, 128, 12), (4099, 1024, 192, 16), (2363392 // 16, 1024, 1024, 16)])
+def test_gemm_mid_bit_identical(M, N, K, P):
+    """Kernel 17 (the mid-K-tile barrier loop: every fragment read overlaps MFMAs that do not wait for it) against the
+    product kernel 1, every epilogue incl. the patch rows, the residual with statistics planes, and the LN fold from
+    12 planes or ViT-L's 16 (the wide path: planes DMA'd at the last K-step): bit-identical, at configs[1]-sized row
+    counts and at the shortest K loops (nk = 1, 2, 3)."""
+    from vitparticlefiltertracker_amd import _lib
+    L = _lib.lib()
+    torch.manual_seed(M + N + K)
+    A = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV) * 0.1
+    R = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    colsum = W.float().sum(1).contiguous()
+    planes_in = torch.stack([torch.randn(P, M, device=DEV) * 3.0, torch.rand(P, M, device=DEV) * 60 + 40], 2)
+    planes_in = planes_in.contiguous()
+    g2 = 196 if M % 196 == 0 else 1
+    pos = torch.randn(g2 + 1, N, device=DEV)
+
+    def run(epi):
+        if epi == 3:
+            out = torch.zeros(M // g2 * (g2 + 1), N, device=DEV, dtype=torch.bfloat16)
+            vpf().gemm(A, W, bias, None, pos, g2, None, None, 3, out)
+            return out, None
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        if epi == 2:
+            out.copy_(R)
+            st = torch.zeros((N + 63) // 64, M, 2, device=DEV)
+            vpf().gemm_stats_(A, W, bias, out, None, 0, 2, out, st)
+            return out, st
+        if epi in (4, 5):
+            vpf().gemm(A, W, bias, None, None, 0, planes_in, colsum, epi, out, P, 1e-6)
+        else:
+            vpf().gemm(A, W, bias, None, None, 0, None, None, epi, out)
+        return out, None
+
+    try:
+        for epi in (0, 1, 2, 3, 4, 5):
+            assert L.vpf_gemm_tune(1, -1) == 0
+            ref, ref_st = run(epi)
+            assert L.vpf_gemm_tune(17, -1) == 0
+            got, st = run(epi)
+            torch.cuda.synchronize()
+            bad = (got.view(torch.int16) != ref.view(torch.int16)).sum().item()
+            assert bad == 0, (epi, bad)
+            if ref_st is not None:
+                assert torch.equal(st, ref_st), epi
+    finally:
+        L.vpf_gemm_tune(0, -1)
 
 
 def test_patch_and_cls_stats_planes():

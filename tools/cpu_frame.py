@@ -25,6 +25,7 @@ def main() -> int:
     ap.add_argument("--arch", default="vit_base_patch16_224")
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--sample-seconds", type=float, default=15.0)
+    ap.add_argument("--batch", type=int, default=8, help="crops per oracle ViT call (bench.py cpu_baseline: 8)")
     args = ap.parse_args()
 
     import numpy as np
@@ -50,10 +51,10 @@ def main() -> int:
     t_start = [0.0]
     feats = ot.features
 
-    def features_with_progress(frame, particles, chunk=64):
+    def features_with_progress(frame, particles, chunk=None):
         out = []
         for i in range(0, particles.shape[1], 256):
-            out.append(feats(frame, np.ascontiguousarray(particles[:, i:i + 256]), chunk))
+            out.append(feats(frame, np.ascontiguousarray(particles[:, i:i + 256]), chunk or args.batch))
             done[0] += out[-1].shape[0]
             print(f"cpu_frame: {done[0]} / {particles.shape[1]} crops, {time.perf_counter() - t_start[0]:.1f} s",
                   file=sys.stderr, flush=True)

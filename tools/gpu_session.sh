@@ -28,6 +28,9 @@ for step in "$@"; do
     attnab)
       timeout -k 10 300 python tools/attn_ab.py $ATTN_VARIANTS > $OUT/attn_ab.log 2>&1
       ok_or_stop $? attnab; cat $OUT/attn_ab.log | grep -v amdgpu.ids ;;
+    gemmab)   # GEMM_VARIANTS e.g. 1,5,17; GEMM_SHAPES e.g. qkv,proj,fc1,fc2
+      timeout -k 10 600 python tools/gemm_ab.py ${GEMM_ROUNDS:-5} ${GEMM_SHAPES:-qkv,proj,fc1,fc2} ${GEMM_VARIANTS:-1,17} > $OUT/gemm_ab.log 2>&1
+      ok_or_stop $? gemmab; grep -v amdgpu.ids $OUT/gemm_ab.log ;;
     pfprobe)
       timeout -k 10 300 python tools/pf_probe.py > $OUT/pf_probe.log 2>&1
       ok_or_stop $? pfprobe; cat $OUT/pf_probe.log | grep particles ;;

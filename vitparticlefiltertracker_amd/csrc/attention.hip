@@ -486,16 +486,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // Q fragments by inline-asm loads: hipcc does not count them, so it cannot merge them into a vmcnt(0) at
     // the first MFMA (which would also drain every K/V chunk). They are older than all DMA pieces, so the
     // first chunk's counted wait retires them; the empty asm after it pins every use below that wait.
-    // 16-query strip: qf[kk] (kk < 2) = Q[32 wid + lane % 16][32 kk + 8 (lane / 16) ..] (attn_step16's B operand).
+    // 16-query strip: qf[kk] (kk < 2) = Q[32 wid + lane % 16][32 kk + 8 (lane / 16) ..] (attn_step16's B operand;
+    // qf[2], qf[3] re-read the same bytes and are unused).
+    // One asm load statement per register for both strip kinds, with the strip kind in the address only: loads issued
+    // in two branches would leave each qf a phi of two asm outputs, and the copies that resolve it run at the branch
+    // merge, before the loads land, so the registers the MFMAs read were stale (the NaNs of round 2's 16-query tail,
+    // on the 32-query strips too).
     bf16x8 qf[4];
-    if (w16) {
-        const bf16_t* qp = qbase + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4);
+    {
+        const bf16_t* qp = w16 ? qbase + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
+                               : qbase + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
+        const int step = w16 ? 32 : 16;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[kk]) : "v"(qp + kk * 32));
-    } else {
-        const bf16_t* qp = qbase + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + ks * 16));
+        for (int ks = 0; ks < 4; ++ks)
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + (w16 ? (ks & 1) : ks) * step));
     }
     {
         const bool isv = wid >= 4;
@@ -510,6 +514,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                                              (lptr_t)(img + g * 1024), 16, 0, 0);
         }
     }
+    // The Q loads are older than this wave's NT DMA pieces: landed once at most NT are outstanding. Wait and pin the
+    // registers HERE, before the strip-kind branch: the compiler copies asm-load destinations wherever register
+    // allocation wants (the phi / live-range copies of the w16 branch below moved qf before any wait, reading stale
+    // registers: the round-2 NaN). The first chunk barrier waits for CPB chunks, so this costs nothing.
+    wait_vmcnt(NT);
+    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
     const bool active = wid < nstrips;
     const int nfull = N >> 5;             // chunks without padded keys
     // The chunk loop, one template for both strip kinds: the barrier schedule (a counted wait + s_barrier before

@@ -54,7 +54,7 @@ constexpr int AUX_BYTES = 2048 + AUX_PARTS * 2048;
 // PART (vpf_gemm_bf16_splitk): blockIdx.y = split s of gridDim.y; the block runs K-tiles [s K/S, (s+1) K/S) and stores
 // its raw fp32 accumulators to the partial plane s ((float*)C + s M N, row-major [M][N]) with no epilogue.
 template <int EPI, bool DEEP, bool WIDE = false, bool OUT8 = false, bool ILV = true, bool PIPED_EPI = true,
-          bool PAR = true, int LAB = 0, bool PART = false>
+          bool PAR = true, int LAB = 0, bool PART = false, bool MID = false>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W,
                                                         const float* __restrict__ bias,
@@ -65,6 +65,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                                                         bf16_t* C, int ldc, int M, int N, int K, int group,
                                                         int stats_parts, float ln_eps, float* stats_out,
                                                         int stats_rows, Out8 o8) {
+    static_assert(!MID || (DEEP && ILV && !PART && LAB == 0), "MID: the deep-ring product kernel's loop only");
     // DEEP: A ring of 3 K-tiles (A prefetched 2 K-tiles ahead: the activation panel is the operand that
     // misses L2), B ring of 2 (weights stay L2-hot); 5 x 32 KiB = all 160 KiB of LDS, and the epilogue
     // operands go into the A slot no K-tile uses any more (slot nk % 3, DMA'd at K-tile max(nk-2, 0)).
@@ -176,7 +177,11 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     // over the 8 waves (12 planes: 3 pieces per wave instead of 12 4-B pieces).
     constexpr bool wide = DEEP && LN && WIDE;   // host: only for stats_parts > AUX_PARTS
     char* planes_lds = wide ? smem + ((nk + 1) % 3) * OPERAND_BYTES : aux + 2048;
+    // The epilogue-operand DMAs re-read the lane id (opaque_lane): their per-lane addresses are then computed where they
+    // are issued (once per tile) instead of being hoisted above the K loop, where MID's register pressure spilled them
+    // and the reload's vmcnt(0) drained the in-flight refills.
     auto load_planes = [&](char* dst) {
+        const int lane = opaque_lane();
         const float* sd = reinterpret_cast<const float*>(stats);
         const int planes = stats_parts > 0 ? stats_parts : 1;
         if ((M & 1) == 0 && ((uintptr_t)sd & 15) == 0) {
@@ -195,6 +200,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     };
     auto load_aux = [&]() {
         if constexpr (PART) return;   // no epilogue operands
+        const int lane = opaque_lane();
         if (wid == 0)
             __builtin_amdgcn_global_load_lds((gptr_t)(bias + min(n0 + lane * 4, N - 4)), (lptr_t)aux, 16, 0, 0);
         if constexpr (LN) {
@@ -212,7 +218,90 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         stage_b(0);
         if (nk > 1) stage_a(1);
     }
-    for (int kt = 0; kt < nk; ++kt) {
+    if constexpr (MID) {
+        // MID: the K-tile's barrier sits between its two 32-deep halves' MFMA blocks, so every fragment read overlaps
+        // MFMAs that do not wait for it. Per K-tile kt (Bar(kt) = the barrier after which tile kt is readable and every
+        // read of tile kt-1 has completed):
+        //   Bar(kt) -> refills B(kt+1), A(kt+2) (the slots of tile kt-1: as kernel 1) -> reads R(kt, ks 0) into F0,
+        //   under MFMA(kt-1, ks 1) on F1 -> wait F0 -> reads R(kt, ks 1) into F1, under MFMA(kt, ks 0) on F0 ->
+        //   wait F1 (every read of tile kt done) -> counted vmcnt + Bar(kt+1) while MFMA(kt, ks 0) drains.
+        // The per-accumulator MFMA order (kt, then ks) is kernel 1's: outputs are bit-identical. Fragment reads are
+        // inline asm (lds16), waited by an lgkmcnt(0) statement naming every destination: hipcc would otherwise put a
+        // vmcnt(0) drain of the in-flight refills in front of reads issued after them.
+        i32x4 fa[2][8], fb[2][4];
+        auto read_half = [&](const char* la_, const char* lb_, int ks) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = wn * 64 + j * 16 + fr;
+                fb[ks][j] = lds16(lb_ + row * 128 + (((ks * 4 + fq) ^ ((row >> 1) & 7)) * 16));
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = wm * 128 + i * 16 + fr;
+                fa[ks][i] = lds16(la_ + row * 128 + (((ks * 4 + fq) ^ ((row >> 1) & 7)) * 16));
+            }
+        };
+        auto wait_half = [&](int ks) {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(fa[ks][0]), "+v"(fa[ks][1]), "+v"(fa[ks][2]), "+v"(fa[ks][3]), "+v"(fa[ks][4]),
+                           "+v"(fa[ks][5]), "+v"(fa[ks][6]), "+v"(fa[ks][7]), "+v"(fb[ks][0]), "+v"(fb[ks][1]),
+                           "+v"(fb[ks][2]), "+v"(fb[ks][3])
+                         :: "memory");
+        };
+        auto mfma_half = [&](int ks) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[ks][j]),
+                                                                        __builtin_bit_cast(bf16x8, fa[ks][i]), acc[j][i],
+                                                                        0, 0, 0);
+        };
+        auto slot_a = [&](int kt) { return (const char*)smem + (kt % 3) * OPERAND_BYTES; };
+        auto slot_b = [&](int kt) { return (const char*)smem + (3 + (kt & 1)) * OPERAND_BYTES; };
+        // Bar(0): A0, B0 landed (A1 may stay in flight)
+        if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        auto iter = [&](int kt, auto first_) {
+            // (after Bar(kt)) the epilogue operands into the A slot no K-tile uses any more, as kernel 1
+            if (kt == (nk >= 2 ? nk - 2 : 0)) load_aux();
+            if (wide && kt == nk - 1) load_planes(planes_lds);
+            read_half(slot_a(kt), slot_b(kt), 0);
+            __builtin_amdgcn_sched_barrier(0);
+            // refills: B(kt+1) -> the B slot of tile kt-1, A(kt+2) -> its A slot (past the end: the last K-tile into
+            // its own slot, identical bytes), one per 4 MFMAs of MFMA(kt-1, ks 1); program order B, A keeps the
+            // counted vmcnt(4) at Bar(kt+1) meaning "B(kt+1) and A(kt+1) have landed"
+            stage_b(min(kt + 1, nk - 1));
+            stage_a(min(kt + 2, nk - 1));
+            if constexpr (!decltype(first_)::value) {
+                mfma_half(1);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            wait_half(0);
+            read_half(slot_a(kt), slot_b(kt), 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_half(0);
+            __builtin_amdgcn_sched_barrier(0);
+            wait_half(1);                                          // every read of tile kt done
+            if (kt + 1 < nk) {
+                if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();                      // Bar(kt+1)
+                asm volatile("" ::: "memory");
+            }
+        };
+        iter(0, std::true_type{});
+        for (int kt = 1; kt < nk; ++kt) iter(kt, std::false_type{});
+        mfma_half(1);                                              // MFMA(nk-1, ks 1)
+    }
+    for (int kt = 0; kt < (MID ? 0 : nk); ++kt) {
         const char* la;
         const char* lb;
         if constexpr (!DEEP) {
@@ -1113,7 +1202,7 @@ constexpr bool kGemmLab = true;
 constexpr bool kGemmLab = false;
 #define VPF_GEMM_LAB_LAUNCH(E)
 #endif
-static bool gemm_kernel_ok(int k) { return k >= 1 && k <= 16 && (kGemmLab || (k != 8 && k != 9)); }
+static bool gemm_kernel_ok(int k) { return k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9)); }
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
         if constexpr (VPF_GEMM_PT_OK(E)) {                                                                   \
@@ -1145,6 +1234,17 @@ static bool gemm_kernel_ok(int k) { return k >= 1 && k <= 16 && (kGemmLab || (k 
                                stats_out, stats_rows, o8);                                                    \
         }                                                                                                    \
         VPF_GEMM_LAB_LAUNCH(E)                                                                               \
+        else if (kern == 17) {                                                                               \
+            if (VPF_IS_LN(E) && stats_parts > AUX_PARTS)                                                     \
+                hipLaunchKernelGGL((k_gemm_bf16<E, true, VPF_IS_LN(E), false, true, true, true, 0, false, true>), \
+                                   grid, block, 0, s, VPF_GEMM_ARGS);                                        \
+            else if (VPF_IS_PROD(E) && o8.q != nullptr)                                                      \
+                hipLaunchKernelGGL((k_gemm_bf16<E, true, false, VPF_IS_PROD(E), true, true, true, 0, false, true>), \
+                                   grid, block, 0, s, VPF_GEMM_ARGS);                                        \
+            else                                                                                             \
+                hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 0, false, true>), grid, \
+                                   block, 0, s, VPF_GEMM_ARGS);                                              \
+        }                                                                                                    \
         else if (kern == 2)                                                                                  \
             hipLaunchKernelGGL((k_gemm_bf16<E, false>), grid, block, 0, s, VPF_GEMM_ARGS);                    \
         else if (kern == 3 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && !(VPF_IS_PROD(E) && o8.q))       \
