@@ -99,7 +99,8 @@ int vpf_gemm_bf16_splitk(const uint16_t* A, int64_t lda, const uint16_t* W, cons
 /* Tuning knob for vpf_gemm_bf16 (process-wide; call it only between launches). kernel: 0 = the per-shape
  * defaults (the ping-pong kernel 5 for VPF_EPI_LN, the deep-ring kernel 1 otherwise; tile group 2 for N <= 1024,
  * 8 for VPF_EPI_LN_GELU, 4 otherwise; group ignored), 1 = the deep-ring kernel (3 A + 2 B K-tiles in LDS) for every shape, 2 = the 2-stage
- * ring (A/B timing; no fp8 output, <= 15 planes), 3-7 and 10-16 = A/B variants (gemm_bf16.hip). group: A-panel group
+ * ring (A/B timing; no fp8 output, <= 15 planes), 3-7 and 10-17 = A/B variants (gemm_bf16.hip; 17 = the mid-K-tile
+ * barrier loop). group: A-panel group
  * size of the tile order for every shape, also used by vpf_gemm_mx8 (0 = row-major; < 0 = keep). Initial values: the
  * per-shape defaults, or VPF_GEMM_KERNEL / VPF_GEMM_GROUP when set. Every accepted kernel gives the same bits.
  * Kernels 8 and 9 (timing probes that do not write C) exist only in a -DVPF_GEMM_LAB build; a product library
