@@ -459,7 +459,9 @@ constexpr int PIPE_CPB = VPF_ATTN_CPB;
 // whose loop took another barrier schedule would release its partners' reads of K / V chunks that have not landed
 // (the round-2 attempt at this tail, which gave its 16-query wave a chunk loop of its own, read such chunks: NaNs
 // on the 32-query strips).
-template <int CPB, bool OUT8 = false, bool TAIL8 = true, bool TAIL16 = true>
+// LAB (lab builds only, VPF_ATTN_LAB): 1 = no Q loads and no K / V DMA (compute on whatever LDS holds: the compute-only
+// time), 2 = loads and barriers only (no key steps: the load-only time).
+template <int CPB, bool OUT8 = false, bool TAIL8 = true, bool TAIL16 = true, int LAB = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_pipe(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows,
     uint8_t* __restrict__ out8 = nullptr, int ld8 = 0, uint8_t* __restrict__ s8 = nullptr, int lds8 = 0) {
@@ -482,6 +484,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int nlast = (N - 1) >> 5;
     const bool w16 = TAIL16 && !OUT8 && wid == nlast && wid < nstrips && N - 32 * nlast <= 16;
 
+    if constexpr (LAB == 3) {   // lab: the second resident workgroup of each CU starts ld8 x ~4k cycles late
+        if (bh >= 256 && bh < 512)
+            for (int i = 0; i < ld8; ++i) __builtin_amdgcn_s_sleep(64);
+    }
     const int q = wid * 32 + l32;
     // Q fragments by inline-asm loads: hipcc does not count them, so it cannot merge them into a vmcnt(0) at
     // the first MFMA (which would also drain every K/V chunk). They are older than all DMA pieces, so the
@@ -497,11 +503,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         const bf16_t* qp = w16 ? qbase + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
                                : qbase + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
         const int step = w16 ? 32 : 16;
+        if constexpr (LAB == 1) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) qf[ks] = bf16x8{(short)(lane + ks), 0x3c00, 0x3c00, 0x3c00, 0, 0, 0, (short)wid};
+        } else {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
             asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + (w16 ? (ks & 1) : ks) * step));
+        }
     }
-    {
+    if constexpr (LAB != 1) {
         const bool isv = wid >= 4;
         const int sub = lane >> 3, slot = lane & 7;
         const bf16_t* src0 = qbase + (isv ? 2 * D : D);
@@ -520,7 +531,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // registers: the round-2 NaN). The first chunk barrier waits for CPB chunks, so this costs nothing.
     wait_vmcnt(NT);
     asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
-    const bool active = wid < nstrips;
+    const bool active = LAB != 2 && wid < nstrips;
     const int nfull = N >> 5;             // chunks without padded keys
     // The chunk loop, one template for both strip kinds: the barrier schedule (a counted wait + s_barrier before
     // chunks 0, CPB, 2 CPB, ..., and before the padded tail chunk) depends on N and CPB only.
@@ -831,8 +842,24 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
                 (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             pipe_attr = true;
         }
-        hipLaunchKernelGGL(fns[2 * tail8 + tail16], dim3((unsigned)(B * H)), dim3(512), lds, (hipStream_t)stream, qkv,
-                           reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows, (uint8_t*)nullptr, 0,
+        pipe_fn fn = fns[2 * tail8 + tail16];
+        int lab_arg = 0;
+#ifdef VPF_GEMM_LAB
+        {   // lab builds: VPF_ATTN_LAB=1 compute only, =2 loads only (timing probes, outputs meaningless)
+            static const pipe_fn lab[3] = {k_attn_bf16_pipe<PIPE_CPB, false, true, true, 1>,
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 2>,
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 3>};
+            const char* le = getenv("VPF_ATTN_LAB");
+            if (le && le[0] >= '1' && le[0] <= '3') {
+                fn = lab[le[0] - '1'];
+                (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            }
+            const char* st = getenv("VPF_ATTN_STAGGER");   // LAB 3's sleep count
+            lab_arg = st ? atoi(st) : 0;
+        }
+#endif
+        hipLaunchKernelGGL(fn, dim3((unsigned)(B * H)), dim3(512), lds, (hipStream_t)stream, qkv,
+                           reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows, (uint8_t*)nullptr, lab_arg,
                            (uint8_t*)nullptr, 0);
         VPF_RETURN_LAUNCH();
     }

@@ -124,6 +124,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     const __amdgpu_buffer_rsrc_t rsB =
         __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * K), (short)0, min(N - n0, BN) * K * 2, 0x00020000);
     uint32_t voffA = 0, voffB = 0;
+    // LAB 5 - 8 (lab kernels 20 - 23): cache-policy bits on the K-loop DMAs (A nt / A sc0 / B nt / A sc1)
+    constexpr int AUXA = LAB == 5 ? 2 : LAB == 6 ? 1 : LAB == 8 ? 16 : 0;
+    constexpr int AUXB = LAB == 7 ? 2 : 0;
     if constexpr (LAB == 4) {
         const int row = 8 * wid + (lane >> 3);
         const int lch = (lane & 7) ^ ((row >> 1) & 7);
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lptr_t)(la + (i * 8 + wid) * 1024), 16, voffA,
                                                          i * 64 * lda * 2 + (int)koff, 0, 0);
             else
-                __builtin_amdgcn_global_load_lds((gptr_t)(Ablk + offA[i] + koff), (lptr_t)(la + (i * 8 + wid) * 1024), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gptr_t)(Ablk + offA[i] + koff), (lptr_t)(la + (i * 8 + wid) * 1024), 16, 0, AUXA);
         }
     };
     auto stage_b = [&](int kt) {   // DEEP: B K-tile kt -> B slot kt & 1
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lptr_t)(lb + (i * 8 + wid) * 1024), 16, voffB,
                                                          i * 64 * K * 2 + (int)koff, 0, 0);
             else
-                __builtin_amdgcn_global_load_lds((gptr_t)(Bblk + offB[i] + koff), (lptr_t)(lb + (i * 8 + wid) * 1024), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gptr_t)(Bblk + offB[i] + koff), (lptr_t)(lb + (i * 8 + wid) * 1024), 16, 0, AUXB);
         }
     };
 
@@ -326,6 +329,10 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         // both 32-deep halves' fragments are read up front (24 ds_read_b128): the second half's reads
         // complete under the first half's 32 MFMAs instead of stalling between them
         bf16x8 a[2][8], b[2][4];
+        // LAB 9 / 10 / 11 (lab kernels 24 / 25 / 26, no epilogue): the K loop with only its DMAs / DMAs + fragment reads /
+        // DMAs + MFMAs on register-resident fragments, to split the loop's time between the three pipes
+        constexpr bool READS = !(LAB == 9 || LAB == 11), MFMAS = !(LAB == 9 || LAB == 10);
+        if constexpr (READS) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -341,6 +348,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                 a[ks][i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + ch * 16);
             }
         }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) b[ks][j] = bf16x8{(short)(fr + j), 1, 2, 3, 4, 5, 6, (short)ks};
+#pragma unroll
+                for (int i = 0; i < 8; ++i) a[ks][i] = bf16x8{(short)(fq + i), 1, 2, 3, 4, 5, 6, (short)ks};
+            }
+        }
         // ILV: the refills are issued from the MFMA block, after the fragment reads in program order (a DMA into
         // LDS is never hoisted over an LDS read; MFMAs may pass it): B(t+1)'s 4 issues right behind the reads,
         // whose latency they overlap, then A(t+2)'s 4 interleaved one per 16 MFMAs, instead of 8 back-to-back
@@ -351,6 +367,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             stage_b(min(kt + 1, nk - 1));
             stage_a(min(kt + 2, nk - 1));
         }
+        if constexpr (MFMAS) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -358,7 +375,17 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
                     acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], a[ks][i], acc[j][i], 0, 0, 0);
-        if constexpr (DEEP && ILV) {
+        } else if constexpr (READS) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(b[ks][j]));
+#pragma unroll
+                for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(a[ks][i]));
+            }
+        }
+        if constexpr (LAB >= 9) {
+        } else if constexpr (DEEP && ILV) {
             __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads
             __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);    // B(t+1)'s DMA
 #pragma unroll
@@ -389,7 +416,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         }
         return;
     }
-    if constexpr (LAB == 2) {
+    if constexpr (LAB == 2 || LAB >= 9) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -1197,12 +1224,39 @@ constexpr bool kGemmLab = true;
                                A, (int)lda, W, bias, residual, pos, patch_rows,                               \
                                reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,        \
                                group | 0x10000, stats_parts, ln_eps, stats_out, stats_rows, o8);              \
+    }                                                                                                        \
+    else if (kern >= 24 && kern <= 26 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {    \
+        if (kern == 24)                                                                                      \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 9>), grid, block, 0, s,   \
+                               VPF_GEMM_ARGS);                                                               \
+        else if (kern == 25)                                                                                 \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 10>), grid, block, 0, s,  \
+                               VPF_GEMM_ARGS);                                                               \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 11>), grid, block, 0, s,  \
+                               VPF_GEMM_ARGS);                                                               \
+    }                                                                                                        \
+    else if (kern >= 20 && kern <= 23 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {    \
+        if (kern == 20)                                                                                      \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 5>), grid, block, 0, s,   \
+                               VPF_GEMM_ARGS);                                                               \
+        else if (kern == 21)                                                                                 \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 6>), grid, block, 0, s,   \
+                               VPF_GEMM_ARGS);                                                               \
+        else if (kern == 22)                                                                                 \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 7>), grid, block, 0, s,   \
+                               VPF_GEMM_ARGS);                                                               \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 8>), grid, block, 0, s,   \
+                               VPF_GEMM_ARGS);                                                               \
     }
 #else
 constexpr bool kGemmLab = false;
 #define VPF_GEMM_LAB_LAUNCH(E)
 #endif
-static bool gemm_kernel_ok(int k) { return k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9)); }
+static bool gemm_kernel_ok(int k) {
+    return (k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9))) || (kGemmLab && k >= 20 && k <= 26);
+}
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
         if constexpr (VPF_GEMM_PT_OK(E)) {                                                                   \
