@@ -79,11 +79,41 @@ __device__ __forceinline__ bf16x4 ds_read_tr_asm_o(uint32_t addr) {
     return r;
 }
 
-template <int T, bool MASK, bool ASM_TR = false>
+#ifndef VPF_ATTN_VEARLY
+#define VPF_ATTN_VEARLY 0
+#endif
+// PRE (ASM_TR only): the four K fragment reads are issued together ahead of the QK^T MFMAs, and the eight V^T reads
+// right behind those MFMAs, so their LDS latency runs under the softmax VALU instead of after it.
+template <int T, bool MASK, bool ASM_TR = false, bool PRE = false>
 __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb, int N, int lane, const bf16x8 qf[4],
                                           float scale_log2, float& m, float& l, f32x16& o0, f32x16& o1) {
+    static_assert(!PRE || (ASM_TR && T == 1), "PRE: the one-tile asm transposed-read step");
     const int l32 = lane & 31, hh = lane >> 5;
     f32x16 s[T];
+    bf16x4 vr[2][2][2];
+    if constexpr (PRE) {
+        s[0] = f32x16{};
+        const int kr = kb + l32;
+        bf16x8 kf[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], qf[ks], s[0], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const int grp = lane >> 4, gi = lane & 15;
+        const int rbase = kb + 4 * (grp >> 1) + (gi >> 2);
+        if constexpr (VPF_ATTN_VEARLY) {   // the first 32-dim column tile's V^T reads (8 VGPRs; both tiles' 16 spill)
+            const int col = 16 * (grp & 1) + 4 * (gi & 3);
+            const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, col >> 3) + (col & 7) * 2);
+            vr[0][0][0] = ds_read_tr_asm_o<0>(a);
+            vr[0][0][1] = ds_read_tr_asm_o<1024>(a);
+            vr[1][0][0] = ds_read_tr_asm_o<2048>(a);
+            vr[1][0][1] = ds_read_tr_asm_o<3072>(a);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    } else {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         s[t] = f32x16{};
@@ -93,6 +123,7 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
             const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
             s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[t], 0, 0, 0);
         }
+    }
     }
     float bm = -INFINITY;
 #pragma unroll
@@ -141,10 +172,9 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
     const int rq = gi >> 2, cp = gi & 3;
     if constexpr (ASM_TR) {
         static_assert(T == 1, "asm transposed-read path handles one 32-key tile");
-        bf16x4 vr[2][2][2];
         const int rbase = kb + 4 * (grp >> 1) + rq;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
+        for (int dt = PRE && VPF_ATTN_VEARLY ? 1 : 0; dt < 2; ++dt) {
             const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
             const int c16 = col >> 3, inner = (col & 7) * 2;
             const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, c16) + inner);
@@ -460,7 +490,8 @@ constexpr int PIPE_CPB = VPF_ATTN_CPB;
 // (the round-2 attempt at this tail, which gave its 16-query wave a chunk loop of its own, read such chunks: NaNs
 // on the 32-query strips).
 // LAB (lab builds only, VPF_ATTN_LAB): 1 = no Q loads and no K / V DMA (compute on whatever LDS holds: the compute-only
-// time), 2 = loads and barriers only (no key steps: the load-only time).
+// time), 2 = loads and barriers only (no key steps: the load-only time), 3 = staggered start (VPF_ATTN_STAGGER),
+// 5 (VPF_ATTN_LAB=4) = the full kernel with the round-2 step order (attn_step without PRE).
 template <int CPB, bool OUT8 = false, bool TAIL8 = true, bool TAIL16 = true, int LAB = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_pipe(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows,
@@ -550,7 +581,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             }
             if (active) {
                 if constexpr (W16) attn_step16<false>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
-                else attn_step<1, false, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                else attn_step<1, false, true, LAB != 5>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
             }
         }
         if (c < NT) {
@@ -562,7 +593,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             if (active) {
                 if constexpr (W16) attn_step16<true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
                 else if (TAIL8 && N - c * 32 <= 8) attn_step_tail8(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-                else attn_step<1, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                else attn_step<1, true, true, LAB != 5>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
             }
         }
     };
@@ -846,11 +877,12 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
         int lab_arg = 0;
 #ifdef VPF_GEMM_LAB
         {   // lab builds: VPF_ATTN_LAB=1 compute only, =2 loads only (timing probes, outputs meaningless)
-            static const pipe_fn lab[3] = {k_attn_bf16_pipe<PIPE_CPB, false, true, true, 1>,
+            static const pipe_fn lab[4] = {k_attn_bf16_pipe<PIPE_CPB, false, true, true, 1>,
                                            k_attn_bf16_pipe<PIPE_CPB, false, true, true, 2>,
-                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 3>};
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 3>,
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 5>};
             const char* le = getenv("VPF_ATTN_LAB");
-            if (le && le[0] >= '1' && le[0] <= '3') {
+            if (le && le[0] >= '1' && le[0] <= '4') {
                 fn = lab[le[0] - '1'];
                 (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             }

@@ -304,6 +304,19 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         for (int kt = 1; kt < nk; ++kt) iter(kt, std::false_type{});
         mfma_half(1);                                              // MFMA(nk-1, ks 1)
     }
+    // LAB 12 (lab kernel 27): an L2 prefetch D = (group >> 17) K-tiles ahead of the DMA stream. At the end of K-step kt
+    // waves 0-3 touch one 128-B line of each of A's 256 rows of K-tile kt + D, waves 4-7 W's (one global_load_dword
+    // per lane into a register nothing reads, kept live to the post-loop vmcnt(0)), so the later LDS-DMA of that
+    // K-tile finds it in L2. The touch is the youngest memory op of its K-step, so the next barrier's counted wait
+    // becomes vmcnt(5).
+    constexpr bool PFE = LAB == 12;
+    const int pfd = PFE ? ((group >> 17) & 15) : 0;
+    int pfreg = 0;
+    const char* pfbase = nullptr;
+    if constexpr (PFE) {
+        const int r = 64 * (wid & 3) + lane;
+        pfbase = wid < 4 ? Ablk + (size_t)min(r, M - 1 - m0) * lda * 2 : Bblk + (size_t)min(r, N - 1 - n0) * K * 2;
+    }
     for (int kt = 0; kt < (MID ? 0 : nk); ++kt) {
         const char* la;
         const char* lb;
@@ -315,8 +328,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         } else {
             // issue order: A0 B0 A1 | per K-tile t: B(t+1) A(t+2). A(kt), B(kt) are older than everything but
             // A(kt+1) (4 pieces per wave) until the last two K-tiles, where the tail is B / aux only.
-            if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (kt + 1 < nk) {
+                if (PFE && kt >= 1 && kt - 1 + pfd < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             if (!ILV && kt + 1 < nk) stage_b(kt + 1);
@@ -384,7 +401,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
                 for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(a[ks][i]));
             }
         }
-        if constexpr (LAB >= 9) {
+        if constexpr (LAB >= 9 && LAB <= 11) {
         } else if constexpr (DEEP && ILV) {
             __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads
             __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);    // B(t+1)'s DMA
@@ -398,6 +415,17 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);   // the 24 fragment reads first
             __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);   // then the 64 MFMAs (counted lgkmcnt waits)
         }
+        if constexpr (PFE) {
+            if (kt + pfd < nk) {
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("global_load_dword %0, %1, off" : "+v"(pfreg) : "v"(pfbase + (uint32_t)(kt + pfd) * 128)
+                             : "memory");
+            }
+        }
+    }
+    if constexpr (PFE) {   // the touches' destination stays reserved until every touch has landed
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        asm volatile("" ::"v"(pfreg));
     }
 
     if constexpr (PART) {
@@ -416,7 +444,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         }
         return;
     }
-    if constexpr (LAB == 2 || LAB >= 9) {
+    if constexpr (LAB == 2 || (LAB >= 9 && LAB <= 11)) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -1212,6 +1240,11 @@ void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__
 // vpf_gemm_tune and ignores them in VPF_GEMM_KERNEL.
 #ifdef VPF_GEMM_LAB
 constexpr bool kGemmLab = true;
+static int gemm_pf_dist() {   // kernel 27's prefetch distance in K-tiles (VPF_GEMM_PFD, default 4)
+    const char* e = getenv("VPF_GEMM_PFD");
+    const int d = e ? atoi(e) : 4;
+    return d < 1 ? 1 : d > 15 ? 15 : d;
+}
 #define VPF_GEMM_LAB_LAUNCH(E)                                                                               \
     else if ((kern == 8 || kern == 9) && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {    \
         if (kern == 8)                                                                                       \
@@ -1224,6 +1257,12 @@ constexpr bool kGemmLab = true;
                                A, (int)lda, W, bias, residual, pos, patch_rows,                               \
                                reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,        \
                                group | 0x10000, stats_parts, ln_eps, stats_out, stats_rows, o8);              \
+    }                                                                                                        \
+    else if (kern == 27 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                 \
+        hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 12>), grid, block, 0, s,      \
+                           A, (int)lda, W, bias, residual, pos, patch_rows,                                   \
+                           reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,            \
+                           group | (gemm_pf_dist() << 17), stats_parts, ln_eps, stats_out, stats_rows, o8);   \
     }                                                                                                        \
     else if (kern >= 24 && kern <= 26 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {    \
         if (kern == 24)                                                                                      \
@@ -1255,7 +1294,7 @@ constexpr bool kGemmLab = false;
 #define VPF_GEMM_LAB_LAUNCH(E)
 #endif
 static bool gemm_kernel_ok(int k) {
-    return (k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9))) || (kGemmLab && k >= 20 && k <= 26);
+    return (k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9))) || (kGemmLab && k >= 20 && k <= 27);
 }
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
