@@ -39,7 +39,7 @@ PEAK_FP8_TFLOPS = 5000.0      # dense block-scaled e4m3 MFMA (same table), the f
 # newest committed PMC summary first (profiles/r<round>_pmc_traffic[_<dtype>].json)
 def _pmc_files(dtype: str):
     suffix = "" if dtype == "bf16" else f"_{dtype}"
-    return [os.path.join(ROOT, "profiles", f"r{r}_pmc_traffic{suffix}.json") for r in (2, 1)]
+    return [os.path.join(ROOT, "profiles", f"r{r}_pmc_traffic{suffix}.json") for r in (3, 2, 1)]
 
 
 def pmc_traffic(arch_name: str, n_local: int, kernel: str, dtype: str = "bf16"):
