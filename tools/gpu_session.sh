@@ -69,6 +69,12 @@ for step in "$@"; do
       ok_or_stop $? pmc8_write
       python tools/pmc_traffic.py $OUT/pmc8_fetch $OUT/pmc8_write --dtype fp8 > $OUT/pmc_traffic_fp8.json 2> $OUT/pmc8_traffic.err
       ok_or_stop $? pmc8_traffic; head -40 $OUT/pmc_traffic_fp8.json ;;
+    bench_c4)   # configs[4]'s per-GPU share: 8192 particles, fp8, 1080p
+      timeout -k 10 900 python bench.py --preset 4 --particles 8192 --steps 5 --warmup 2 --cpu-seconds 0 > $OUT/bench_c4.log 2>&1
+      ok_or_stop $? bench_c4; tail -1 $OUT/bench_c4.log | cut -c1-400 ;;
+    bench_p512)   # the 8-GPU share of the 4096-particle frame
+      timeout -k 10 600 python bench.py --particles 512 --steps 10 --warmup 3 --cpu-seconds 0 > $OUT/bench_p512.log 2>&1
+      ok_or_stop $? bench_p512; tail -1 $OUT/bench_p512.log | cut -c1-400 ;;
     bench8)
       timeout -k 10 900 python bench.py --dtype fp8 --steps 5 --warmup 2 --cpu-seconds 0 > $OUT/bench8.log 2>&1
       ok_or_stop $? bench8; tail -1 $OUT/bench8.log | cut -c1-600 ;;

@@ -79,6 +79,9 @@ __device__ __forceinline__ bf16x4 ds_read_tr_asm_o(uint32_t addr) {
     return r;
 }
 
+#ifndef VPF_ATTN_SWP_UNROLL
+#define VPF_ATTN_SWP_UNROLL 0
+#endif
 #ifndef VPF_ATTN_VEARLY
 #define VPF_ATTN_VEARLY 0
 #endif
@@ -282,6 +285,109 @@ __device__ __forceinline__ void attn_step_tail8(const char* Ks, const char* Vs, 
         if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o0, 0, 0, 0);
         else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o1, 0, 0, 0);
     }
+}
+
+// Software-pipelined form of the 32-query key step, split in two halves so that QK^T of chunk c + 1 is issued
+// before the softmax of chunk c: its four MFMAs then run under that softmax's VALU instead of on the step's
+// critical path (the step was QK^T -> wait -> max -> exp -> PV in one wave). Same operations in the same order per
+// accumulator as attn_step<1, MASK, true, true> / attn_step_tail8: the results are bit-identical.
+__device__ __forceinline__ int lane_id_opaque() {   // not hoistable: the address math stays in the step using it
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    return lane;
+}
+__device__ __forceinline__ f32x16 attn_qk32(const char* Ks, int kb, int lane, const bf16x8 qf[4]) {
+    lane = lane_id_opaque();
+    const int l32 = lane & 31, hh = lane >> 5;
+    const int kr = kb + l32;
+    bf16x8 kf[4];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
+    f32x16 s = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], qf[ks], s, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);   // issued here, ahead of the softmax that follows: they run under it
+    return s;
+}
+// MODE 0: a full chunk; 1: the masked last chunk (keys >= N get probability 0); 2: the last chunk when at most 8 of
+// its keys are real (attn_step_tail8's work: 4 live scores per lane, the second 16-key PV half skipped).
+template <int MODE>
+__device__ __forceinline__ void attn_sm_pv32(const char* Vs, int kb, int N, int lane, f32x16 s, float scale_log2,
+                                             float& m, float& l, f32x16& o0, f32x16& o1) {
+    lane = lane_id_opaque();
+    const int hh = lane >> 5;
+    constexpr int NR = MODE == 2 ? 4 : 16;
+    float bm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        if constexpr (MODE != 0) {
+            const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= N) s[r] = -INFINITY;
+        }
+        bm = fmaxf(bm, s[r]);
+    }
+    bm = xor32_max(bm);
+    if (__builtin_expect(__any(bm > m + 8.0f / scale_log2), 0)) {
+        const float mn = fmaxf(m, bm);
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            o0[r] *= alpha;
+            o1[r] *= alpha;
+        }
+    }
+    const float msc = m * scale_log2;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], scale_log2, -msc));
+        s[r] = p;
+        l += p;
+    }
+    bf16x8 pf[2];
+    if constexpr (MODE == 2) {
+        pf[0] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(s[0], s[1]), pack_bf2(s[2], s[3]), 0u, 0u));
+    } else {
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+            pf[st] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(s[8 * st + 0], s[8 * st + 1]),
+                                                           pack_bf2(s[8 * st + 2], s[8 * st + 3]),
+                                                           pack_bf2(s[8 * st + 4], s[8 * st + 5]),
+                                                           pack_bf2(s[8 * st + 6], s[8 * st + 7])));
+    }
+    const int grp = lane >> 4, gi = lane & 15;
+    const int rbase = kb + 4 * (grp >> 1) + (gi >> 2);
+    constexpr int NST = MODE == 2 ? 1 : 2;
+    bf16x4 vr[2][2][2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * (grp & 1) + 4 * (gi & 3);
+        const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, col >> 3) + (col & 7) * 2);
+        vr[0][dt][0] = ds_read_tr_asm_o<0>(a);
+        vr[0][dt][1] = ds_read_tr_asm_o<1024>(a);
+        if constexpr (NST == 2) {
+            vr[1][dt][0] = ds_read_tr_asm_o<2048>(a);
+            vr[1][dt][1] = ds_read_tr_asm_o<3072>(a);
+        }
+    }
+    if constexpr (NST == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1]),
+                     "+v"(vr[1][0][0]), "+v"(vr[1][0][1]), "+v"(vr[1][1][0]), "+v"(vr[1][1][1])::"memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1])
+                     ::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int st = 0; st < NST; ++st)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const bf16x4 lo = vr[st][dt][0], hi = vr[st][dt][1];
+            const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o0, 0, 0, 0);
+            else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o1, 0, 0, 0);
+        }
 }
 
 // 16-query strip on v_mfma_f32_16x16x32_bf16: the last strip when it holds at most 16 real queries (N = 197 ->
@@ -563,6 +669,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     wait_vmcnt(NT);
     asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
     const bool active = LAB != 2 && wid < nstrips;
+    constexpr bool SWP = LAB == 6;   // lab: the software-pipelined 32-query strip (VPF_ATTN_LAB=5)
     const int nfull = N >> 5;             // chunks without padded keys
     // The chunk loop, one template for both strip kinds: the barrier schedule (a counted wait + s_barrier before
     // chunks 0, CPB, 2 CPB, ..., and before the padded tail chunk) depends on N and CPB only.
@@ -572,6 +679,41 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             if constexpr (W16) asm volatile("" : "+v"(qf[0]), "+v"(qf[1]) :: "memory");
             else asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
         };
+        if constexpr (!W16 && SWP) {
+            // software-pipelined 32-query strip: the barrier before chunk group g (chunks g CPB ..) is taken before
+            // QK^T of chunk g CPB, i.e. in iteration g CPB - 1; the same barriers in the same order as below
+            if (!active) {   // a wave without a strip passes the same barriers
+                for (int c = 0; c < NT; c += CPB) {
+                    wait_vmcnt(max(NT - c - CPB, 0));
+                    __builtin_amdgcn_s_barrier();
+                }
+                return;
+            }
+            wait_vmcnt(max(NT - CPB, 0));
+            __builtin_amdgcn_s_barrier();
+            pin_q();
+            // full chunks c < nfull; the tail chunk (c = nfull < NT) is peeled. (Unrolled by two, to alternate the
+            // score tiles without the 8 v_mov_b64 of `cur = nxt`, hipcc spills 20-75 VGPRs at the 128 limit.)
+            f32x16 cur = attn_qk32(Ks, 0, lane, qf);
+            for (int c = 0; c < nfull; ++c) {
+                f32x16 nxt;
+                if (c + 1 < NT) {
+                    if ((c + 1) % CPB == 0) {
+                        wait_vmcnt(max(NT - (c + 1) - CPB, 0));
+                        __builtin_amdgcn_s_barrier();
+                        pin_q();
+                    }
+                    nxt = attn_qk32(Ks, (c + 1) * 32, lane, qf);
+                }
+                attn_sm_pv32<0>(Vs, c * 32, N, lane, cur, scale_log2, m, l, o0, o1);
+                cur = nxt;
+            }
+            if (nfull < NT) {
+                if (TAIL8 && N - nfull * 32 <= 8) attn_sm_pv32<2>(Vs, nfull * 32, N, lane, cur, scale_log2, m, l, o0, o1);
+                else attn_sm_pv32<1>(Vs, nfull * 32, N, lane, cur, scale_log2, m, l, o0, o1);
+            }
+            return;
+        }
         int c = 0;
         for (; c < nfull; ++c) {
             if (c % CPB == 0) {   // chunks c .. c+CPB-1 landed for every wave
@@ -877,12 +1019,13 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
         int lab_arg = 0;
 #ifdef VPF_GEMM_LAB
         {   // lab builds: VPF_ATTN_LAB=1 compute only, =2 loads only (timing probes, outputs meaningless)
-            static const pipe_fn lab[4] = {k_attn_bf16_pipe<PIPE_CPB, false, true, true, 1>,
+            static const pipe_fn lab[5] = {k_attn_bf16_pipe<PIPE_CPB, false, true, true, 1>,
                                            k_attn_bf16_pipe<PIPE_CPB, false, true, true, 2>,
                                            k_attn_bf16_pipe<PIPE_CPB, false, true, true, 3>,
-                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 5>};
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 5>,
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 6>};
             const char* le = getenv("VPF_ATTN_LAB");
-            if (le && le[0] >= '1' && le[0] <= '4') {
+            if (le && le[0] >= '1' && le[0] <= '5') {
                 fn = lab[le[0] - '1'];
                 (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             }
