@@ -75,6 +75,10 @@ for step in "$@"; do
     bench_p512)   # the 8-GPU share of the 4096-particle frame
       timeout -k 10 600 python bench.py --particles 512 --steps 10 --warmup 3 --cpu-seconds 0 > $OUT/bench_p512.log 2>&1
       ok_or_stop $? bench_p512; tail -1 $OUT/bench_p512.log | cut -c1-400 ;;
+    prof_c4)   # rocprofv3 kernel stats of configs[4]'s per-GPU share
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof_c4 -o run --output-format csv -- python3 bench.py --preset 4 --particles 8192 --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/prof_c4.log 2>&1
+      ok_or_stop $? prof_c4; tail -1 $OUT/prof_c4.log | cut -c1-300 ;;
     bench8)
       timeout -k 10 900 python bench.py --dtype fp8 --steps 5 --warmup 2 --cpu-seconds 0 > $OUT/bench8.log 2>&1
       ok_or_stop $? bench8; tail -1 $OUT/bench8.log | cut -c1-600 ;;
