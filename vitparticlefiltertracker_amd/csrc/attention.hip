@@ -79,10 +79,7 @@ __device__ __forceinline__ bf16x4 ds_read_tr_asm_o(uint32_t addr) {
     return r;
 }
 
-#ifndef VPF_ATTN_SWP_UNROLL
-#define VPF_ATTN_SWP_UNROLL 0
-#endif
-#ifndef VPF_ATTN_VEARLY
+#ifndef VPF_ATTN_VEARLY   // -DVPF_ATTN_VEARLY=1: PRE also issues the first V^T tile's reads early (spills; A/B only)
 #define VPF_ATTN_VEARLY 0
 #endif
 // PRE (ASM_TR only): the four K fragment reads are issued together ahead of the QK^T MFMAs, and the eight V^T reads
