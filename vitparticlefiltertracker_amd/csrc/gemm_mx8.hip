@@ -46,7 +46,9 @@ __device__ __forceinline__ void mx_col(f32x4 (&acc)[8], const i32x8& b, const i3
 }
 #undef VPF_MX
 
-template <int EPI, bool OUT8, bool EARLY = true>
+// LAB (lab builds only, VPF_MX8_VARIANT 7 / 8 / 9): 1 = no epilogue (the K loop alone), 2 = the loop's DMAs and
+// barriers only, 3 = DMAs + fragment reads (no MFMAs). Timing probes: they do not write C.
+template <int EPI, bool OUT8, bool EARLY = true, int LAB = 0>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict__ A, int lda,
                                                        const uint32_t* __restrict__ As, int lds_a,
                                                        const uint8_t* __restrict__ W,
@@ -151,6 +153,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
         // halves), and the scale of K-block b = [32b, 32b+32) comes from lane group b. So a lane reads logical
         // chunks fq and 4+fq of its row, and supplies the scale of block fq: one word per 64-row brick, byte f
         // = fragment f of the brick (mx8_scale_byte).
+        if constexpr (LAB == 2) {
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            stage(kt & 1, min(kt + 2, nk - 1));
+            continue;
+        }
         i32x4 bl[4], bh[4], al[8], ah[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -178,6 +186,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
                      : "+v"(al[0]), "+v"(al[1]), "+v"(al[2]), "+v"(al[3]), "+v"(al[4]), "+v"(al[5]), "+v"(al[6]),
                        "+v"(al[7]), "+v"(ah[0]), "+v"(ah[1]), "+v"(ah[2]), "+v"(ah[3]), "+v"(ah[4]), "+v"(ah[5]),
                        "+v"(ah[6]), "+v"(ah[7]));
+        if constexpr (LAB == 3) {
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            stage(kt & 1, min(kt + 2, nk - 1));
+            continue;
+        }
         i32x8 a[8], b[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -219,6 +233,13 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
         __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing refills land before the ring is reused
+    if constexpr (LAB != 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(acc[j][i]));
+        return;
+    }
 
     if constexpr (LN) {
         if (stats_parts > 0 && tid < BM) {   // planes -> {mean, rstd} once per row (see gemm_bf16.hip)
@@ -276,8 +297,17 @@ __global__ __launch_bounds__(256) void k_quantize_mx8(const bf16_t* __restrict__
 #define VPF_MX8_ARGS                                                                                         \
     A, (int)lda, As, (int)lds_a, W, Ws, bias, residual, reinterpret_cast<const float2*>(row_stats), colsum,    \
         C, (int)ldc, (int)M, (int)N, (int)K, group, stats_parts, ln_eps, stats_out, o8
+#ifdef VPF_GEMM_LAB
+#define VPF_MX8_LAB_LAUNCH(E)                                                                                \
+        if (labv == 1) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 1>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 2) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 2>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 3) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 3>), grid, block, 0, s, VPF_MX8_ARGS); break; }
+#else
+#define VPF_MX8_LAB_LAUNCH(E)
+#endif
 #define VPF_MX8_LAUNCH(E)                                                                                    \
     do {                                                                                                     \
+        VPF_MX8_LAB_LAUNCH(E)                                                                                \
         if (o8.q && late)                                                                                    \
             hipLaunchKernelGGL((k_gemm_mx8<E, true, false>), grid, block, 0, s, VPF_MX8_ARGS);                \
         else if (o8.q)                                                                                       \
@@ -316,6 +346,8 @@ VPF_API int vpf_gemm_mx8(const uint8_t* A, int64_t lda, const uint32_t* As, int6
     // VPF_MX8_VARIANT=0: the previous schedule (all MFMAs after the buffer-release barrier), for A/B timing
     const char* var = getenv("VPF_MX8_VARIANT");
     const bool late = var && var[0] == '0';
+    const int labv = var && var[0] >= '7' && var[0] <= '9' ? var[0] - '6' : 0;   // lab builds: 7 / 8 / 9 -> LAB 1 / 2 / 3
+    (void)labv;
     switch (epilogue) {
         case VPF_EPI_BIAS: VPF_MX8_LAUNCH(VPF_EPI_BIAS); break;
         case VPF_EPI_BIAS_GELU: VPF_MX8_LAUNCH(VPF_EPI_BIAS_GELU); break;
