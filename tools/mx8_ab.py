@@ -65,6 +65,20 @@ def main():
             fns["mx8_v" + v] = fv
         if os.environ.get("AB_NO_BF16"):   # variant A/B only: the bf16 call's own operands would cool the MALL
             fns.pop("bf16")
+        for v in [x for x in os.environ.get("AB_CHECK", "").split(",") if x]:   # bit-equality of full-kernel variants
+            def snap():
+                torch.cuda.synchronize()
+                return [t.clone() for t in (out, q8, s8) if t is not None]
+            if name == "fc2":
+                out.copy_(out0 := (torch.rand(M, N, device=dev, generator=g) * 2 - 1).to(torch.bfloat16))
+            f8()
+            ref = snap()
+            if name == "fc2":
+                out.copy_(out0)
+            fns["mx8_v" + v]()
+            got = snap()
+            same = all(torch.equal(x, y) for x, y in zip(ref, got))
+            print(f"{name:4s} variant {v} bit-identical to the product schedule: {same}", flush=True)
         for f in fns.values():
             f()
         torch.cuda.synchronize()
