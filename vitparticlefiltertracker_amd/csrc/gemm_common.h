@@ -480,5 +480,87 @@ __device__ __forceinline__ void store_wave_tile_q8(char* img, const char* aux, c
                                           (lane & 15)] = word;
 }
 
+// Pipelined form of store_wave_tile_q8 (same bits): row group i's LN / GELU math and image rows, then that group's
+// quantise + 16-B element stores, so the stores start after the first 16 rows instead of after all 128 and drain
+// under the remaining math (store_wave_tile_pipe's order, for the fp8-only output).
+template <int EPI>
+__device__ __forceinline__ void store_wave_tile_q8_pipe(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm,
+                                                        int wn, int m0, int n0, int lane, int M, int N, Out8 o8) {
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    const int fr = lane & 15, fq = lane >> 4, cc = lane & 3;
+    float4 bv[4], cv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = (wn * 64 + j * 16 + fq * 4) * 4;
+        bv[j] = *reinterpret_cast<const float4*>(aux + c);
+        if constexpr (LN) cv[j] = *reinterpret_cast<const float4*>(aux + 1024 + c);
+    }
+    uint32_t e8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        f32x2 rsx = {1.f, 1.f}, rsy = {0.f, 0.f};
+        if constexpr (LN) {
+            const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + (wm * 128 + i * 16 + fr) * 8);
+            rsx = f32x2{st.y, st.y};
+            rsy = f32x2{-st.y * st.x, -st.y * st.x};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f32x2 v01, v23;
+            const f32x2 a01 = {acc[j][i][0], acc[j][i][1]}, a23 = {acc[j][i][2], acc[j][i][3]};
+            const f32x2 b01 = {bv[j].x, bv[j].y}, b23 = {bv[j].z, bv[j].w};
+            if constexpr (LN) {
+                const f32x2 c01 = {cv[j].x, cv[j].y}, c23 = {cv[j].z, cv[j].w};
+                v01 = __builtin_elementwise_fma(rsx, a01, __builtin_elementwise_fma(rsy, c01, b01));
+                v23 = __builtin_elementwise_fma(rsx, a23, __builtin_elementwise_fma(rsy, c23, b23));
+            } else {
+                v01 = a01 + b01;
+                v23 = a23 + b23;
+            }
+            if constexpr (EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU) {
+                v01 = gelu_sig2(v01);
+                v23 = gelu_sig2(v23);
+            }
+            const int row = i * 16 + fr;
+            const int c8 = (j * 4 + fq) ^ (row & 15);
+            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) = make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
+        }
+        __builtin_amdgcn_wave_barrier();   // the image is private to this wave: its LDS ops stay in order
+        const int row = i * 16 + (lane >> 2);
+        uint4 h[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c16 = 2 * cc + u;
+            uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+            if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+            h[u] = v;
+        }
+        uint32_t am = max(mx8_amax8(h[0]), mx8_amax8(h[1]));
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0xB1, 0xF, 0xF, false));   // lane pair = block
+        const int E = mx8_block_exp(am);
+        e8[i] = (uint32_t)(E + 127);
+        const uint2 q0 = mx8_pack8(h[0], E), q1 = mx8_pack8(h[1], E);
+        const int m = m0 + wm * 128 + row;
+        const int n = n0 + wn * 64 + cc * 16;
+        if (m < M && n < N) *reinterpret_cast<uint4*>(o8.q + (int64_t)m * o8.ldq + n) = make_uint4(q0.x, q0.y, q1.x, q1.y);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if ((lane & 1) == 0) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int row = it * 16 + (lane >> 2);
+            const int w = (row >> 6) * 32 + (cc >> 1) * 16 + (row & 15);
+            img[w * 4 + ((row >> 4) & 3)] = (char)e8[it];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t word = *reinterpret_cast<const uint32_t*>(img + lane * 4);
+    const int nb = n0 + wn * 64;
+    const int R = m0 + wm * 128 + (lane >> 5) * 64;   // brick row base
+    if (nb < N && R < o8.lds)
+        reinterpret_cast<uint32_t*>(o8.s)[(int64_t)(nb >> 7) * o8.lds + R + (((nb >> 5) & 3) + ((lane >> 4) & 1)) * 16 +
+                                          (lane & 15)] = word;
+}
+
 }  // namespace gemm
 }  // namespace vpf

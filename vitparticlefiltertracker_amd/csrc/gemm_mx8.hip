@@ -333,11 +333,17 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
     __builtin_amdgcn_s_barrier();   // the ring is free: 8 x 16 KiB epilogue images
     asm volatile("" ::: "memory");
     float* prod_stats = EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr;
-    if (OUT8 && C == nullptr)   // fp8-only output (FC1): 16-B element stores, gathered scale words
-        store_wave_tile_q8<EPI>(smem + wid * 16384, aux, acc, wm, wn, m0, n0, lane, M, N, o8);
-    else
-        store_wave_tile<EPI, OUT8>(smem + wid * 16384, aux, acc, wm, wn, m0, n0, lane, res, nullptr, 1, C, ldc,
-                                   M, N, prod_stats, M, o8);
+    char* img = smem + wid * 16384;
+    if (OUT8 && C == nullptr) {   // fp8-only output (FC1): 16-B element stores, gathered scale words
+        if constexpr (LAB == 5) store_wave_tile_q8_pipe<EPI>(img, aux, acc, wm, wn, m0, n0, lane, M, N, o8);
+        else store_wave_tile_q8<EPI>(img, aux, acc, wm, wn, m0, n0, lane, M, N, o8);
+        return;
+    }
+    if constexpr (LAB == 5 && !OUT8 && EPI != VPF_EPI_BIAS_RESIDUAL) {   // bf16 output only (QKV): the pipelined pass
+        store_wave_tile_pipe<EPI>(img, aux, acc, wm, wn, m0, n0, lane, res, C, ldc, M, N, nullptr, 0);
+        return;
+    }
+    store_wave_tile<EPI, OUT8>(img, aux, acc, wm, wn, m0, n0, lane, res, nullptr, 1, C, ldc, M, N, prod_stats, M, o8);
 }
 
 // MX quantisation of bf16 rows: one lane per 8 values, a DPP quad per 32-value block (gemm_common.h).
@@ -372,7 +378,9 @@ __global__ __launch_bounds__(256) void k_quantize_mx8(const bf16_t* __restrict__
         if (labv == 2) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 2>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
         if (labv == 3) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 3>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
         if (labv == 4 && o8.q) { hipLaunchKernelGGL((k_gemm_mx8<E, true, true, 4>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
-        if (labv == 4) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 4>), grid, block, 0, s, VPF_MX8_ARGS); break; }
+        if (labv == 4) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 4>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 5 && o8.q) { hipLaunchKernelGGL((k_gemm_mx8<E, true, true, 5>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 5) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 5>), grid, block, 0, s, VPF_MX8_ARGS); break; }
 #else
 #define VPF_MX8_LAB_LAUNCH(E)
 #endif
@@ -418,7 +426,8 @@ VPF_API int vpf_gemm_mx8(const uint8_t* A, int64_t lda, const uint32_t* As, int6
     const char* var = getenv("VPF_MX8_VARIANT");
     const bool late = var && var[0] == '0';
     // lab builds: 7 / 8 / 9 -> LAB 1 / 2 / 3 (probes), 6 -> LAB 4 (row-major schedule, full kernel)
-    const int labv = var && var[0] >= '7' && var[0] <= '9' ? var[0] - '6' : var && var[0] == '6' ? 4 : 0;
+    const int labv = var && var[0] >= '7' && var[0] <= '9' ? var[0] - '6' : var && var[0] == '6' ? 4
+                     : var && var[0] == '5' ? 5 : 0;   // 5 -> LAB 5: the pipelined fp8-only epilogue
     (void)labv;
     switch (epilogue) {
         case VPF_EPI_BIAS: VPF_MX8_LAUNCH(VPF_EPI_BIAS); break;
