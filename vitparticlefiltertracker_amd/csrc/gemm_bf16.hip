@@ -1017,7 +1017,8 @@ __device__ __forceinline__ void mfma_zero(f32x4& c, const i32x4& w, const i32x4&
 
 // BAL: A(t+2) is issued in phase A of K-tile t (8 pieces per phase) instead of A(t+3) in phase B; the prologue then
 // stages A0 B0 A1 B1 and the vmcnt count at Y_t is the same (A(t+2), issued after B(t+1)... see phase_a).
-template <int EPI, bool OUT8 = false, bool BAL = true>
+// NOEPI (lab kernel 28): the K loop alone, no epilogue (timing probe; C not written).
+template <int EPI, bool OUT8 = false, bool BAL = true, bool NOEPI = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, const float* __restrict__ bias,
                const bf16_t* residual, const float* __restrict__ pos, int g2, const float2* __restrict__ stats,
@@ -1186,6 +1187,10 @@ void k_gemm_w4(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__
             asm volatile("" : "+a"(acc[h][j][0]), "+a"(acc[h][j][1]), "+a"(acc[h][j][2]), "+a"(acc[h][j][3]),
                          "+a"(acc[h][j][4]), "+a"(acc[h][j][5]), "+a"(acc[h][j][6]), "+a"(acc[h][j][7]));
 
+    if constexpr (NOEPI) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        return;
+    }
     // ---------------- epilogue ----------------
     if constexpr (LN) {
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the epilogue operands landed ...
@@ -1258,6 +1263,9 @@ static int gemm_pf_dist() {   // kernel 27's prefetch distance in K-tiles (VPF_G
                                reinterpret_cast<const float2*>(row_stats), colsum, C, (int)ldc, m, n, k,        \
                                group | 0x10000, stats_parts, ln_eps, stats_out, stats_rows, o8);              \
     }                                                                                                        \
+    else if (kern == 28 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                 \
+        hipLaunchKernelGGL((k_gemm_w4<E, false, true, true>), grid, dim3(256), 0, s, VPF_GEMM_ARGS);           \
+    }                                                                                                        \
     else if (kern == 27 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                 \
         hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 12>), grid, block, 0, s,      \
                            A, (int)lda, W, bias, residual, pos, patch_rows,                                   \
@@ -1294,7 +1302,7 @@ constexpr bool kGemmLab = false;
 #define VPF_GEMM_LAB_LAUNCH(E)
 #endif
 static bool gemm_kernel_ok(int k) {
-    return (k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9))) || (kGemmLab && k >= 20 && k <= 27);
+    return (k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9))) || (kGemmLab && k >= 20 && k <= 28);
 }
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
