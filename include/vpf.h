@@ -103,10 +103,11 @@ int vpf_gemm_bf16_splitk(const uint16_t* A, int64_t lda, const uint16_t* W, cons
  * barrier loop). group: A-panel group
  * size of the tile order for every shape, also used by vpf_gemm_mx8 (0 = row-major; < 0 = keep). Initial values: the
  * per-shape defaults, or VPF_GEMM_KERNEL / VPF_GEMM_GROUP when set. Every accepted kernel gives the same bits.
- * Kernels 8, 9 and 24-26 (timing probes that do not write C: no stores / no epilogue / only the K loop's DMAs,
- * DMAs + fragment reads, DMAs + MFMAs) and 20-23 (cache-policy bits on the K-loop DMAs; same bits as kernel 1) exist
- * only in a -DVPF_GEMM_LAB build (make lab -> libvpf_lab.so); a product library returns VPF_ERR_ARG for them, as for
- * an unknown kernel, and ignores them in VPF_GEMM_KERNEL. */
+ * Kernels 8, 9, 24-26 and 28 (timing probes that do not write C: no stores / no epilogue / only the K loop's DMAs,
+ * DMAs + fragment reads, DMAs + MFMAs / the 4-wave loop alone), 20-23 (cache-policy bits on the K-loop DMAs) and 27
+ * (an L2 prefetch ahead of the DMAs; both same bits as kernel 1) exist only in a -DVPF_GEMM_LAB build (make lab ->
+ * libvpf_lab.so); a product library returns VPF_ERR_ARG for them, as for an unknown kernel, and ignores them in
+ * VPF_GEMM_KERNEL. */
 int vpf_gemm_tune(int kernel, int group);
 
 /* MX8 operands (OCP MX-FP8: e4m3fn elements, one e8m0 scale per 32 consecutive K values):

@@ -190,7 +190,7 @@ def test_gemm_tune_rejects_lab_only_kernels():
     try:
         assert L.vpf_gemm_tune(8, -1) == -1 and L.vpf_gemm_tune(9, -1) == -1
         assert L.vpf_gemm_tune(18, -1) == -1 and L.vpf_gemm_tune(-2, -1) == -1
-        for k in (20, 23, 24, 26):                     # lab-build-only probes
+        for k in (20, 23, 24, 26, 27, 28):             # lab-build-only probes
             assert L.vpf_gemm_tune(k, -1) == -1
         for k in (1, 5, 7, 10, 13, 16, 17):
             assert L.vpf_gemm_tune(k, -1) == 0
