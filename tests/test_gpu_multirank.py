@@ -83,3 +83,61 @@ def test_sharded_tracker_equals_single_rank(world, P):
                 f"rank {r} frame {k}: particle states"
     for k in range(FRAMES):
         assert all(out[r][k][0] == out[0][k][0] for r in range(world)), f"frame {k + 1}: ranks disagree"
+
+
+# ------------------------------------------------------------------ MultiTracker across ranks (§8f rank 4)
+BOXES = [(40, 50, 48, 48), (120, 100, 56, 40)]
+
+
+def _mt_run(mt, clip):
+    out = []
+    mt.init(clip[0], BOXES)
+    for f in clip[1:]:
+        ests = mt.track(f)
+        out.append((ests, [pf.last_ancestors.cpu().numpy().copy() for pf in mt.pfs],
+                    [pf.particles.cpu().numpy().copy() for pf in mt.pfs]))
+    return out
+
+
+def _mt_worker(rank, world, port, P, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vitparticlefiltertracker_amd import MultiTracker
+        from vitparticlefiltertracker_amd.frames import synthetic_clip
+        mt = MultiTracker(_cfg(P), n_objects=len(BOXES), device="cuda:0", rank=rank, world_size=world)
+        q.put((rank, _mt_run(mt, synthetic_clip(FRAMES + 1))))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,P", [(2, 128), (3, 33)])
+def test_sharded_multitracker_equals_single_rank(world, P):
+    """Two targets, each target's particles sharded over the ranks: every rank returns the single-rank
+    MultiTracker's estimates bit for bit, and its shards of every target's ancestors and states."""
+    from vitparticlefiltertracker_amd import MultiTracker
+    from vitparticlefiltertracker_amd.frames import synthetic_clip
+    ref = _mt_run(MultiTracker(_cfg(P), n_objects=len(BOXES), device="cuda:0"), synthetic_clip(FRAMES + 1))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mt_worker, args=(r, world, port, P, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = P // world
+    for r in range(world):
+        assert not isinstance(out[r], str), out[r]
+        for k, ((ests, ancs, parts), (ests1, ancs1, parts1)) in enumerate(zip(out[r], ref), start=1):
+            assert ests == ests1, f"rank {r} frame {k}: estimates {ests} vs single rank {ests1}"
+            for t in range(len(BOXES)):
+                assert np.array_equal(ancs[t], ancs1[t][r * n:(r + 1) * n]), f"rank {r} frame {k} target {t}"
+                assert np.array_equal(parts[t].view(np.uint32), parts1[t][:, r * n:(r + 1) * n].view(np.uint32))

@@ -275,23 +275,34 @@ class MultiTracker:
     ViT forward over every target's particles per frame (crops with each target's own template box, one patch
     GEMM / encoder / final LN over all K*P crops, cosine weights against each target's own template), captured
     into one HIP graph. Target k's particle stream is seeded with particles.seed + k, so a MultiTracker with one
-    target reproduces Tracker bit for bit. Single GPU (world size 1)."""
+    target reproduces Tracker bit for bit.
+    Several ranks (as Tracker): every target's particles are sharded by index range over the ranks, each rank runs
+    the ViT over its K x P/G crops, and each target's filter does its own chunk all-gather + global estimate /
+    resample, so every rank returns the same K estimates, bit-identical to one rank."""
 
-    def __init__(self, cfg=None, n_objects: int = 1, device=None, use_graph: bool = True, weights=None):
+    def __init__(self, cfg=None, n_objects: int = 1, device=None, use_graph: bool = True, weights=None,
+                 rank: Optional[int] = None, world_size: Optional[int] = None, group=None):
         self.cfg = load_config(cfg)
         if not torch.cuda.is_available():
             raise _lib.VPFError("MultiTracker runs on the HIP device only")
         if n_objects < 1:
             raise ValueError("n_objects >= 1")
-        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.rank, self.world_size, self.group = _dist_info(rank, world_size, group)
+        if device is None:
+            local = int(os.environ.get("LOCAL_RANK", self.rank % max(1, torch.cuda.device_count())))
+            device = torch.device("cuda", local)
+        self.device = torch.device(device)
         torch.cuda.set_device(self.device)
         c = self.cfg
         self.arch = arch_of(c)
         self.K = int(n_objects)
         self.P = int(c["particles"]["num"])
+        if self.P % self.world_size:
+            raise ValueError("particles.num must be divisible by the world size")
+        self.n_local = self.P // self.world_size
         w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
-        self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, self.K * self.P, c["model"]["mean"],
-                                c["model"]["std"])
+        self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, self.K * self.n_local,
+                                c["model"]["mean"], c["model"]["std"])
         self.lam = float(c["likelihood"]["lambda"])
         self.bits = int(c["likelihood"]["weight_bits"])
         self.use_graph = bool(use_graph)
@@ -326,7 +337,8 @@ class MultiTracker:
             self.boxes.append((bw, bh))
             self.pfs.append(ParticleFilter(self.P, (cx, cy, 1.0), c["particles"]["motion_std"],
                                            c["particles"]["scale_range"], int(c["particles"]["seed"]) + k,
-                                           self.device, (fd.shape[0], fd.shape[1]), self.lam, self.bits))
+                                           self.device, (fd.shape[0], fd.shape[1]), self.lam, self.bits,
+                                           self.rank, self.world_size, self.group))
         self._graph = None
         self.frame_index = 0
 
@@ -335,7 +347,7 @@ class MultiTracker:
         n = eng.embed_many(self._frame_dev, [pf.particles for pf in self.pfs], self.boxes)
         eng.encoder(n)
         for k in range(self.K):
-            eng.weights_from_tokens(self.P, self.templates[k], self.lam, self.bits, row0=k * self.P)
+            eng.weights_from_tokens(self.n_local, self.templates[k], self.lam, self.bits, row0=k * self.n_local)
 
     def _capture(self) -> None:
         s = torch.cuda.Stream(device=self.device)
@@ -365,7 +377,7 @@ class MultiTracker:
         else:
             self._forward()
         for k, pf in enumerate(self.pfs):       # every target's estimate + resample enqueued, then one wait
-            pf.set_weights(self.engine.Q[k * self.P:(k + 1) * self.P])
+            pf.set_weights(self.engine.Q[k * self.n_local:(k + 1) * self.n_local])
             pf._settle()
             pf._commit()
         return [pf._read_estimate() for pf in self.pfs]
