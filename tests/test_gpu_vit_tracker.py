@@ -53,9 +53,10 @@ def test_vit_features_vs_oracle(name, dtype, n):
 
 @pytest.mark.parametrize("name,dtype", [("vit_base_patch16_224", "bf16"), ("vit_small_patch16_224", "fp8"),
                                         ("vit_large_patch14_336", "bf16")])
-def test_cls_fused_tail_equals_kv_path(name, dtype, monkeypatch):
+def test_cls_fused_tail_equals_kv_path(name, dtype):
     """The last block's CLS attention without K / V (vpf_cls_attn_fold_bf16 between two block-diagonal GEMMs)
-    against the K / V GEMM + attention path it replaces (VPF_CLS_FUSED=0), and both against the fp32 oracle."""
+    against the K / V GEMM + attention path it replaces (ViTEngine(cls_fused=False)), and both against the fp32
+    oracle."""
     from vitparticlefiltertracker_amd.vit import ViTEngine
     arch = ARCHS[name]
     w = make_vit_weights(arch, seed=6, perturb_affine=True)
@@ -65,8 +66,7 @@ def test_cls_fused_tail_equals_kv_path(name, dtype, monkeypatch):
     fused = ViTEngine(arch, w, dtype, DEV, n)
     assert fused.cls_fused
     f1 = fused.features(fd, pd, (64.0, 64.0)).double().cpu()
-    monkeypatch.setenv("VPF_CLS_FUSED", "0")
-    plain = ViTEngine(arch, w, dtype, DEV, n)
+    plain = ViTEngine(arch, w, dtype, DEV, n, cls_fused=False)
     assert not plain.cls_fused
     f0 = plain.features(fd, pd, (64.0, 64.0)).double().cpu()
     cos = torch.nn.functional.cosine_similarity(f1, f0, dim=1)

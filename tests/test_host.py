@@ -180,19 +180,31 @@ def test_checkpoint_paths_round_trip():
         assert f == want and t._checkpoint_file(f) == f
 
 
-def test_gemm_tune_rejects_lab_only_kernels():
-    """the timing probes that never write C (kernels 8 / 9) are not in the product library, so a stray
-    vpf_gemm_tune call cannot turn every GEMM into garbage; real variants are still accepted (host state only)."""
+def test_product_library_has_no_knobs():
+    """the product libvpf.so holds only the kernels it dispatches and reads no environment variable.
+    * it imports no getenv (so VPF_GEMM_KERNEL=3, VPF_ATTN_TAIL16=0, VPF_MX8_VARIANT, VPF_CROP_LDS, ... cannot change
+      a product launch: nothing reads them);
+    * none of the lab kernels (persistent / four-wave GEMMs, the attention's software-pipelined strip) is in its code
+      object; they live in the lab build (tools/gemm_lab);
+    * vpf_gemm_tune accepts only the two product bf16 kernels (1, 5) and 0 (the per-shape defaults)."""
+    import subprocess
     from vitparticlefiltertracker_amd import _lib
     if not os.path.exists(_lib.LIB_PATH):
         _lib.build()
+    dyn = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert "getenv" not in dyn and "secure_getenv" not in dyn, dyn
+    blob = open(_lib.LIB_PATH, "rb").read()
+    for lab_kernel in (b"k_gemm_pt", b"k_gemm_w4", b"attn_qk32", b"attn_sm_pv32", b"k_crop_patches_fast"):
+        assert lab_kernel not in blob, lab_kernel
+    for product_kernel in (b"k_gemm_bf16", b"k_gemm_pp", b"k_gemm_mx8", b"k_attn_bf16_pipe", b"k_crop_patches_lds"):
+        assert product_kernel in blob, product_kernel
     L = _lib.lib()
     try:
-        assert L.vpf_gemm_tune(8, -1) == -1 and L.vpf_gemm_tune(9, -1) == -1
-        assert L.vpf_gemm_tune(18, -1) == -1 and L.vpf_gemm_tune(-2, -1) == -1
-        for k in (20, 23, 24, 26, 27, 28):             # lab-build-only probes
-            assert L.vpf_gemm_tune(k, -1) == -1
-        for k in (1, 5, 7, 10, 13, 16, 17):
+        for k in (2, 3, 4, 6, 7, 8, 9, 10, 13, 16, 17, 18, 20, 24, 27, 28, -2):
+            assert L.vpf_gemm_tune(k, -1) == -1, k
+        for k in (1, 5):
             assert L.vpf_gemm_tune(k, -1) == 0
+        assert L.vpf_gemm_tune(1, 999) == -1
     finally:
         assert L.vpf_gemm_tune(0, -1) == 0

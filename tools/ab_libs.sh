@@ -1,6 +1,7 @@
 #!/bin/bash
-# Build A/B variants of libvpf.so into ab_libs/ (travels to the GPU box; git-ignored): attention chunks-per-barrier
-# (cpbN), the crop's LDS window size in dwords (cropN) or the GEMM's MFMAs per A-refill issue (ilvN).
+# Build A/B variants of libvpf.so into ab_libs/ (travels to the GPU box; git-ignored): the crop's LDS window size in
+# dwords (cropN). The attention chunks-per-barrier (VPF_ATTN_CPB) and GEMM refill-spacing (VPF_ILV_SPACING) macros of
+# rounds 1-3 are in the lab snapshots (tools/gemm_lab/*_lab.hip); the product sources fix them (6 and 16).
 # usage: bash tools/ab_libs.sh cpb2 crop10240 ...   then  VPF_LIB_PATH=ab_libs/libvpf_cpb2.so python bench.py ...
 set -e
 cd "$(dirname "$0")/.."
@@ -9,9 +10,7 @@ C=vitparticlefiltertracker_amd/csrc
 F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -fvisibility=hidden"
 for v in "$@"; do
   case $v in
-    cpb*) src=attention; def="-DVPF_ATTN_CPB=${v#cpb}" ;;
     crop*) src=crop; def="-DVPF_CROP_LDS_DW=${v#crop}" ;;
-    ilv*) src=gemm_bf16; def="-DVPF_ILV_SPACING=${v#ilv}" ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
   OBJS=""

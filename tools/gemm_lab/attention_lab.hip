@@ -15,6 +15,7 @@
 //
 // fp32 parity path (vpf_attention_f32): one thread per query, K/V of the head in LDS as fp32, exact
 // expf softmax (N <= 256).
+#include <cstdlib>
 #include <type_traits>
 
 #include "vpf_common.h"
@@ -78,8 +79,11 @@ __device__ __forceinline__ bf16x4 ds_read_tr_asm_o(uint32_t addr) {
     return r;
 }
 
-// PRE (ASM_TR only): the four K fragment reads are issued together ahead of the QK^T MFMAs (one lgkmcnt wait instead of
-// four read -> wait -> MFMA pairs; profiles/r3_lab/attn_pre_stagger_ab.txt).
+#ifndef VPF_ATTN_VEARLY   // -DVPF_ATTN_VEARLY=1: PRE also issues the first V^T tile's reads early (spills; A/B only)
+#define VPF_ATTN_VEARLY 0
+#endif
+// PRE (ASM_TR only): the four K fragment reads are issued together ahead of the QK^T MFMAs, and the eight V^T reads
+// right behind those MFMAs, so their LDS latency runs under the softmax VALU instead of after it.
 template <int T, bool MASK, bool ASM_TR = false, bool PRE = false>
 __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb, int N, int lane, const bf16x8 qf[4],
                                           float scale_log2, float& m, float& l, f32x16& o0, f32x16& o1) {
@@ -97,6 +101,17 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
         for (int ks = 0; ks < 4; ++ks) s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], qf[ks], s[0], 0, 0, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const int grp = lane >> 4, gi = lane & 15;
+        const int rbase = kb + 4 * (grp >> 1) + (gi >> 2);
+        if constexpr (VPF_ATTN_VEARLY) {   // the first 32-dim column tile's V^T reads (8 VGPRs; both tiles' 16 spill)
+            const int col = 16 * (grp & 1) + 4 * (gi & 3);
+            const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, col >> 3) + (col & 7) * 2);
+            vr[0][0][0] = ds_read_tr_asm_o<0>(a);
+            vr[0][0][1] = ds_read_tr_asm_o<1024>(a);
+            vr[1][0][0] = ds_read_tr_asm_o<2048>(a);
+            vr[1][0][1] = ds_read_tr_asm_o<3072>(a);
+        }
         __builtin_amdgcn_sched_barrier(0);
     } else {
 #pragma unroll
@@ -159,7 +174,7 @@ __device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb
         static_assert(T == 1, "asm transposed-read path handles one 32-key tile");
         const int rbase = kb + 4 * (grp >> 1) + rq;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
+        for (int dt = PRE && VPF_ATTN_VEARLY ? 1 : 0; dt < 2; ++dt) {
             const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
             const int c16 = col >> 3, inner = (col & 7) * 2;
             const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, c16) + inner);
@@ -267,6 +282,109 @@ __device__ __forceinline__ void attn_step_tail8(const char* Ks, const char* Vs, 
         if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o0, 0, 0, 0);
         else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o1, 0, 0, 0);
     }
+}
+
+// Software-pipelined form of the 32-query key step, split in two halves so that QK^T of chunk c + 1 is issued
+// before the softmax of chunk c: its four MFMAs then run under that softmax's VALU instead of on the step's
+// critical path (the step was QK^T -> wait -> max -> exp -> PV in one wave). Same operations in the same order per
+// accumulator as attn_step<1, MASK, true, true> / attn_step_tail8: the results are bit-identical.
+__device__ __forceinline__ int lane_id_opaque() {   // not hoistable: the address math stays in the step using it
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    return lane;
+}
+__device__ __forceinline__ f32x16 attn_qk32(const char* Ks, int kb, int lane, const bf16x8 qf[4]) {
+    lane = lane_id_opaque();
+    const int l32 = lane & 31, hh = lane >> 5;
+    const int kr = kb + l32;
+    bf16x8 kf[4];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
+    f32x16 s = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], qf[ks], s, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);   // issued here, ahead of the softmax that follows: they run under it
+    return s;
+}
+// MODE 0: a full chunk; 1: the masked last chunk (keys >= N get probability 0); 2: the last chunk when at most 8 of
+// its keys are real (attn_step_tail8's work: 4 live scores per lane, the second 16-key PV half skipped).
+template <int MODE>
+__device__ __forceinline__ void attn_sm_pv32(const char* Vs, int kb, int N, int lane, f32x16 s, float scale_log2,
+                                             float& m, float& l, f32x16& o0, f32x16& o1) {
+    lane = lane_id_opaque();
+    const int hh = lane >> 5;
+    constexpr int NR = MODE == 2 ? 4 : 16;
+    float bm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        if constexpr (MODE != 0) {
+            const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= N) s[r] = -INFINITY;
+        }
+        bm = fmaxf(bm, s[r]);
+    }
+    bm = xor32_max(bm);
+    if (__builtin_expect(__any(bm > m + 8.0f / scale_log2), 0)) {
+        const float mn = fmaxf(m, bm);
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            o0[r] *= alpha;
+            o1[r] *= alpha;
+        }
+    }
+    const float msc = m * scale_log2;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], scale_log2, -msc));
+        s[r] = p;
+        l += p;
+    }
+    bf16x8 pf[2];
+    if constexpr (MODE == 2) {
+        pf[0] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(s[0], s[1]), pack_bf2(s[2], s[3]), 0u, 0u));
+    } else {
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+            pf[st] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(s[8 * st + 0], s[8 * st + 1]),
+                                                           pack_bf2(s[8 * st + 2], s[8 * st + 3]),
+                                                           pack_bf2(s[8 * st + 4], s[8 * st + 5]),
+                                                           pack_bf2(s[8 * st + 6], s[8 * st + 7])));
+    }
+    const int grp = lane >> 4, gi = lane & 15;
+    const int rbase = kb + 4 * (grp >> 1) + (gi >> 2);
+    constexpr int NST = MODE == 2 ? 1 : 2;
+    bf16x4 vr[2][2][2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * (grp & 1) + 4 * (gi & 3);
+        const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, col >> 3) + (col & 7) * 2);
+        vr[0][dt][0] = ds_read_tr_asm_o<0>(a);
+        vr[0][dt][1] = ds_read_tr_asm_o<1024>(a);
+        if constexpr (NST == 2) {
+            vr[1][dt][0] = ds_read_tr_asm_o<2048>(a);
+            vr[1][dt][1] = ds_read_tr_asm_o<3072>(a);
+        }
+    }
+    if constexpr (NST == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1]),
+                     "+v"(vr[1][0][0]), "+v"(vr[1][0][1]), "+v"(vr[1][1][0]), "+v"(vr[1][1][1])::"memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1])
+                     ::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int st = 0; st < NST; ++st)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const bf16x4 lo = vr[st][dt][0], hi = vr[st][dt][1];
+            const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o0, 0, 0, 0);
+            else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o1, 0, 0, 0);
+        }
 }
 
 // 16-query strip on v_mfma_f32_16x16x32_bf16: the last strip when it holds at most 16 real queries (N = 197 ->
@@ -462,7 +580,10 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // heads, profiles/r1_gemm_lab/attn_cpb.txt): each barrier puts all 8 waves back in lockstep. Round 2 on the current
 // kernel (profiles/r2_gemm_lab/attn_cpb_r2s5.txt, per-launch averages from bench.py): CPB 3 / 4 / 5 / 6 / 7 =
 // 1.084 / 1.075 / 1.069 / 1.064 / 1.156 ms at N = 197; 6 and 4 are level on ViT-L (N = 577) and on the MX8 output.
-constexpr int PIPE_CPB = 6;
+#ifndef VPF_ATTN_CPB
+#define VPF_ATTN_CPB 6   // -DVPF_ATTN_CPB=n builds A/B variants (tools/ab_libs.sh)
+#endif
+constexpr int PIPE_CPB = VPF_ATTN_CPB;
 // OUT8: the output is written as MX8 (the fp8 path's proj A operand) instead of bf16: the same packed bf16
 // values, quantised per 32-dim block (a block = 16 dims of a lane + 16 of its partner half-wave lane).
 // TAIL16: when the last strip holds at most 16 real queries (q_rows % 32 in 1..16: N = 197), its wave runs the
@@ -471,10 +592,10 @@ constexpr int PIPE_CPB = 6;
 // whose loop took another barrier schedule would release its partners' reads of K / V chunks that have not landed
 // (the round-2 attempt at this tail, which gave its 16-query wave a chunk loop of its own, read such chunks: NaNs
 // on the 32-query strips).
-// TAIL8: the last key step runs attn_step_tail8 when at most 8 of its keys are real.
-// The round-3 lab variants of this kernel (compute-only / load-only probes, staggered start, software-pipelined strip,
-// the round-2 step order) are in the lab build (tools/gemm_lab/attention_lab.hip).
-template <int CPB, bool OUT8 = false>
+// LAB (lab builds only, VPF_ATTN_LAB): 1 = no Q loads and no K / V DMA (compute on whatever LDS holds: the compute-only
+// time), 2 = loads and barriers only (no key steps: the load-only time), 3 = staggered start (VPF_ATTN_STAGGER),
+// 5 (VPF_ATTN_LAB=4) = the full kernel with the round-2 step order (attn_step without PRE).
+template <int CPB, bool OUT8 = false, bool TAIL8 = true, bool TAIL16 = true, int LAB = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_pipe(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows,
     uint8_t* __restrict__ out8 = nullptr, int ld8 = 0, uint8_t* __restrict__ s8 = nullptr, int lds8 = 0) {
@@ -495,8 +616,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // wave-uniform: this wave's strip holds query N - 1 and at most 16 real queries. Decided by N, not q_rows, so a
     // row's result does not depend on how many rows the call computes.
     const int nlast = (N - 1) >> 5;
-    constexpr bool TAIL8 = true;
-    const bool w16 = !OUT8 && wid == nlast && wid < nstrips && N - 32 * nlast <= 16;
+    const bool w16 = TAIL16 && !OUT8 && wid == nlast && wid < nstrips && N - 32 * nlast <= 16;
+
+    if constexpr (LAB == 3) {   // lab: the second resident workgroup of each CU starts ld8 x ~4k cycles late
+        if (bh >= 256 && bh < 512)
+            for (int i = 0; i < ld8; ++i) __builtin_amdgcn_s_sleep(64);
+    }
     const int q = wid * 32 + l32;
     // Q fragments by inline-asm loads: hipcc does not count them, so it cannot merge them into a vmcnt(0) at
     // the first MFMA (which would also drain every K/V chunk). They are older than all DMA pieces, so the
@@ -512,11 +637,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         const bf16_t* qp = w16 ? qbase + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
                                : qbase + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
         const int step = w16 ? 32 : 16;
+        if constexpr (LAB == 1) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) qf[ks] = bf16x8{(short)(lane + ks), 0x3c00, 0x3c00, 0x3c00, 0, 0, 0, (short)wid};
+        } else {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
             asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + (w16 ? (ks & 1) : ks) * step));
+        }
     }
-    {
+    if constexpr (LAB != 1) {
         const bool isv = wid >= 4;
         const int sub = lane >> 3, slot = lane & 7;
         const bf16_t* src0 = qbase + (isv ? 2 * D : D);
@@ -532,21 +662,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // The Q loads are older than this wave's NT DMA pieces: landed once at most NT are outstanding. Wait and pin the
     // registers HERE, before the strip-kind branch: the compiler copies asm-load destinations wherever register
     // allocation wants (the phi / live-range copies of the w16 branch below moved qf before any wait, reading stale
-    // registers: the round-2 NaN). The wait and the pin are ONE statement, so no copy of qf can be placed
-    // between them; the loads are the only earlier statements that write qf. The first chunk barrier waits for CPB
-    // chunks, so this costs nothing.
-    switch (NT) {   // NT = ceil(N / 32) <= 8 (N <= 256); the immediate must be a constant
-#define VPF_QWAIT(k)                                                                                             \
-    case k:                                                                                                      \
-        asm volatile("s_waitcnt vmcnt(" #k ")" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory"); \
-        break;
-        VPF_QWAIT(1) VPF_QWAIT(2) VPF_QWAIT(3) VPF_QWAIT(4) VPF_QWAIT(5) VPF_QWAIT(6) VPF_QWAIT(7) VPF_QWAIT(8)
-#undef VPF_QWAIT
-        default:
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
-            break;
-    }
-    const bool active = wid < nstrips;
+    // registers: the round-2 NaN). The first chunk barrier waits for CPB chunks, so this costs nothing.
+    wait_vmcnt(NT);
+    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+    const bool active = LAB != 2 && wid < nstrips;
+    constexpr bool SWP = LAB == 6;   // lab: the software-pipelined 32-query strip (VPF_ATTN_LAB=5)
     const int nfull = N >> 5;             // chunks without padded keys
     // The chunk loop, one template for both strip kinds: the barrier schedule (a counted wait + s_barrier before
     // chunks 0, CPB, 2 CPB, ..., and before the padded tail chunk) depends on N and CPB only.
@@ -556,6 +676,41 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             if constexpr (W16) asm volatile("" : "+v"(qf[0]), "+v"(qf[1]) :: "memory");
             else asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
         };
+        if constexpr (!W16 && SWP) {
+            // software-pipelined 32-query strip: the barrier before chunk group g (chunks g CPB ..) is taken before
+            // QK^T of chunk g CPB, i.e. in iteration g CPB - 1; the same barriers in the same order as below
+            if (!active) {   // a wave without a strip passes the same barriers
+                for (int c = 0; c < NT; c += CPB) {
+                    wait_vmcnt(max(NT - c - CPB, 0));
+                    __builtin_amdgcn_s_barrier();
+                }
+                return;
+            }
+            wait_vmcnt(max(NT - CPB, 0));
+            __builtin_amdgcn_s_barrier();
+            pin_q();
+            // full chunks c < nfull; the tail chunk (c = nfull < NT) is peeled. (Unrolled by two, to alternate the
+            // score tiles without the 8 v_mov_b64 of `cur = nxt`, hipcc spills 20-75 VGPRs at the 128 limit.)
+            f32x16 cur = attn_qk32(Ks, 0, lane, qf);
+            for (int c = 0; c < nfull; ++c) {
+                f32x16 nxt;
+                if (c + 1 < NT) {
+                    if ((c + 1) % CPB == 0) {
+                        wait_vmcnt(max(NT - (c + 1) - CPB, 0));
+                        __builtin_amdgcn_s_barrier();
+                        pin_q();
+                    }
+                    nxt = attn_qk32(Ks, (c + 1) * 32, lane, qf);
+                }
+                attn_sm_pv32<0>(Vs, c * 32, N, lane, cur, scale_log2, m, l, o0, o1);
+                cur = nxt;
+            }
+            if (nfull < NT) {
+                if (TAIL8 && N - nfull * 32 <= 8) attn_sm_pv32<2>(Vs, nfull * 32, N, lane, cur, scale_log2, m, l, o0, o1);
+                else attn_sm_pv32<1>(Vs, nfull * 32, N, lane, cur, scale_log2, m, l, o0, o1);
+            }
+            return;
+        }
         int c = 0;
         for (; c < nfull; ++c) {
             if (c % CPB == 0) {   // chunks c .. c+CPB-1 landed for every wave
@@ -565,7 +720,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             }
             if (active) {
                 if constexpr (W16) attn_step16<false>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
-                else attn_step<1, false, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                else attn_step<1, false, true, LAB != 5>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
             }
         }
         if (c < NT) {
@@ -577,7 +732,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             if (active) {
                 if constexpr (W16) attn_step16<true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
                 else if (TAIL8 && N - c * 32 <= 8) attn_step_tail8(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-                else attn_step<1, true, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                else attn_step<1, true, true, LAB != 5>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
             }
         }
     };
@@ -810,6 +965,18 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ qkv,
 
 }  // namespace
 
+static int cu_count() {
+    static int cached = 0;
+    if (!cached) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cached = n;
+        else
+            cached = 256;
+    }
+    return cached;
+}
+
 VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd, float scale,
                                int q_rows, void* stream) {
     if (B < 0 || N <= 0 || N > 640 || H <= 0 || hd != HD || B * H > INT32_MAX || q_rows < 1 || q_rows > N)
@@ -825,18 +992,47 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
                            N, H, (int)BH, scale_log2);
         VPF_RETURN_LAUNCH();
     }
-    // N <= 256: the key-pipelined kernel (8 waves, one strip each); N > 256: the whole-image kernel (waves loop over
-    // strips)
-    if (N <= 256) {
+    // N <= 256: the key-pipelined kernel (8 waves, one strip each). VPF_ATTN_MODE=0 selects the
+    // whole-image kernel instead (A/B timing); N > 256 always takes it (waves loop over strips).
+    const char* mode = getenv("VPF_ATTN_MODE");
+    if (N <= 256 && !(mode && mode[0] == '0')) {
+        // VPF_ATTN_TAIL=0: the general masked last step instead of attn_step_tail8; VPF_ATTN_TAIL16=0: the last
+        // strip as a 32-query strip even when it holds <= 16 queries (A/B timing; every variant is tested)
+        const char* tail = getenv("VPF_ATTN_TAIL");
+        const char* t16 = getenv("VPF_ATTN_TAIL16");
+        const bool tail8 = !(tail && tail[0] == '0'), tail16 = !(t16 && t16[0] == '0');
+        typedef void (*pipe_fn)(const bf16_t*, bf16_t*, int, int, float, int, uint8_t*, int, uint8_t*, int);
+        static const pipe_fn fns[4] = {k_attn_bf16_pipe<PIPE_CPB, false, false, false>,
+                                       k_attn_bf16_pipe<PIPE_CPB, false, false, true>,
+                                       k_attn_bf16_pipe<PIPE_CPB, false, true, false>,
+                                       k_attn_bf16_pipe<PIPE_CPB, false, true, true>};
         static bool pipe_attr = false;   // benign race: idempotent attribute set
         if (!pipe_attr) {
-            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, false>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            for (pipe_fn f : fns)
+                (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             pipe_attr = true;
         }
-        hipLaunchKernelGGL((k_attn_bf16_pipe<PIPE_CPB, false>), dim3((unsigned)(B * H)), dim3(512), lds,
-                           (hipStream_t)stream, qkv, reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows,
-                           (uint8_t*)nullptr, 0, (uint8_t*)nullptr, 0);
+        pipe_fn fn = fns[2 * tail8 + tail16];
+        int lab_arg = 0;
+#ifdef VPF_GEMM_LAB
+        {   // lab builds: VPF_ATTN_LAB=1 compute only, =2 loads only (timing probes, outputs meaningless)
+            static const pipe_fn lab[5] = {k_attn_bf16_pipe<PIPE_CPB, false, true, true, 1>,
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 2>,
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 3>,
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 5>,
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 6>};
+            const char* le = getenv("VPF_ATTN_LAB");
+            if (le && le[0] >= '1' && le[0] <= '5') {
+                fn = lab[le[0] - '1'];
+                (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            }
+            const char* st = getenv("VPF_ATTN_STAGGER");   // LAB 3's sleep count
+            lab_arg = st ? atoi(st) : 0;
+        }
+#endif
+        hipLaunchKernelGGL(fn, dim3((unsigned)(B * H)), dim3(512), lds, (hipStream_t)stream, qkv,
+                           reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows, (uint8_t*)nullptr, lab_arg,
+                           (uint8_t*)nullptr, 0);
         VPF_RETURN_LAUNCH();
     }
     const int threads = 64 * (strips < 8 ? strips : 8);

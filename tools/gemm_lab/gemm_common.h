@@ -160,22 +160,26 @@ __device__ __forceinline__ void epi_to_image(char* img, const char* aux, const f
 }
 
 // Pipelined form of epi_to_image + store_wave_tile for the epilogues with a bf16 output only (EPI_BIAS / BIAS_GELU /
-// LN / LN_GELU / BIAS_RESIDUAL with its statistics planes): fragment row-group i's math and image rows, then that
-// group's two 16-B store iterations, so the stores start after the first 16 rows instead of after all 128 and drain
-// under the remaining math. Same image layout as the two-pass form (bit-identical output).
-// Store iteration h of group i covers the group's rows of parity h (rows i*16 + 2*(lane/8) + h; still 8 rows x 128 B
-// per instruction), so the 8-B half swap that the image swizzle applies to odd rows is resolved at compile time instead
-// of by 4 v_cndmask per chunk, and stores / residual loads address from one per-lane base pointer plus a wave-uniform
-// row offset instead of a 64-bit multiply-add each (profiles/r2_gemm_lab/epilogue_parity_rows_ab.txt).
-template <int EPI>
+// LN / LN_GELU / BIAS_RESIDUAL with its statistics planes): fragment row-group i's math and image rows, then that group's two 16-B store iterations, so
+// the stores start after the first 16 rows instead of after all 128 and drain under the remaining math. Same image
+// layout as the two-pass form (bit-identical output).
+// PAR: store iteration h of group i covers the group's rows of parity h (rows i*16 + 2*(lane/8) + h; still 8 rows
+// x 128 B per instruction), so the 8-B half swap that the image swizzle applies to odd rows is resolved at compile
+// time instead of by 4 v_cndmask per chunk, and stores / residual loads address from one per-lane base pointer
+// plus a wave-uniform row offset instead of a 64-bit multiply-add each. !PAR: the original row order (A/B, kernel 6).
+// IMG16: the image holds one 16-row group (2 KiB per wave, rows indexed mod 16) instead of the wave's 128 rows: the
+// persistent kernel's epilogue, whose free LDS is the next tile's operand ring. Not with the residual statistics.
+template <int EPI, bool PAR = true, bool CHK = false, bool IMG16 = false>   // CHK: C == nullptr skips the C stores (A/B)
 __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm,
                                                      int wn, int m0, int n0, int lane, const uint4 (&res)[16],
                                                      bf16_t* C, int ldc, int M, int N, float* stats_out,
                                                      int stats_rows) {
     constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
     constexpr bool RES = EPI == VPF_EPI_BIAS_RESIDUAL;
+    static_assert(!(RES && IMG16), "the residual statistics partials need the whole 128-row image");
+    constexpr int RMASK = IMG16 ? 15 : 127;
     const int fr = lane & 15, fq = lane >> 4, c16 = lane & 7;
-    // the lane's store pointer at row offset 0 of the wave tile (only dereferenced where ok)
+    // PAR: the lane's store pointer at row offset 0 of the wave tile (only dereferenced where ok)
     bf16_t* Cl = C + (int64_t)(m0 + wm * 128 + 2 * (lane >> 3)) * ldc + (n0 + wn * 64 + c16 * 8);
     float4 bv[4], cv[4];
 #pragma unroll
@@ -211,15 +215,15 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
             }
             const int row = i * 16 + fr;
             const int c8 = (j * 4 + fq) ^ (row & 15);
-            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) =
+            *reinterpret_cast<uint2*>(img + (row & RMASK) * 128 + c8 * 8) =
                 make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
         }
         __builtin_amdgcn_wave_barrier();   // the image is private to this wave: LDS ops of one wave stay in order
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int row = i * 16 + 2 * (lane >> 3) + h;   // rows of group i only
-            uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
-            if (h == 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+            const int row = PAR ? i * 16 + 2 * (lane >> 3) + h : (2 * i + h) * 8 + (lane >> 3);   // rows of group i only
+            uint4 v = *reinterpret_cast<const uint4*>(img + (row & RMASK) * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+            if (PAR ? (h == 1) : (row & 1) != 0) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
             const int m = m0 + wm * 128 + row;
             const int n = n0 + wn * 64 + c16 * 8;
             const bool ok = m < M && n < N;
@@ -247,7 +251,10 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
                     *reinterpret_cast<float2*>(img + row * 128 + c16 * 8) = make_float2(s1, s2);
                 }
             }
-            if (ok) *reinterpret_cast<uint4*>(Cl + (int64_t)(i * 16 + h) * ldc) = v;
+            if (ok && (!CHK || C != nullptr)) {
+                if constexpr (PAR) *reinterpret_cast<uint4*>(Cl + (int64_t)(i * 16 + h) * ldc) = v;
+                else *reinterpret_cast<uint4*>(C + (int64_t)m * ldc + n) = v;
+            }
         }
     }
     if constexpr (RES) {
@@ -273,8 +280,8 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
 // The residual rows a lane adds in store_wave_tile (EPI_BIAS_RESIDUAL): 16 x 16 B, all in flight at once. The
 // kernels issue this right after their K loop, before the epilogue barrier (a raw s_barrier, so the loads stay
 // in flight across it), which gives them the LN combine, the barrier and the image writes to land under.
-// PAR: the row order of store_wave_tile_pipe (res[2i + h] = row i*16 + 2*(lane/8) + h), from one per-lane base
-// pointer; !PAR: row it*8 + lane/8 (store_wave_tile).
+// PAR: the row order of store_wave_tile_pipe<EPI, true> (res[2i + h] = row i*16 + 2*(lane/8) + h), from one per-lane
+// base pointer; !PAR: row it*8 + lane/8 (store_wave_tile, store_wave_tile_pipe<EPI, false>).
 template <bool PAR = true>
 __device__ __forceinline__ void load_residual(uint4 (&res)[16], const bf16_t* residual, int wm, int wn, int m0,
                                               int n0, int lane, int ldc, int M, int N) {
@@ -455,6 +462,88 @@ __device__ __forceinline__ void store_wave_tile_q8(char* img, const char* aux, c
     }
     // scale bytes -> the wave's 64 words (word w = brick (w >> 5), block (w >> 4) & 1, row r16 = w & 15; byte f =
     // rows 16f + r16 of the brick), staged in image bytes no lane reads any more
+    __builtin_amdgcn_wave_barrier();
+    if ((lane & 1) == 0) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int row = it * 16 + (lane >> 2);
+            const int w = (row >> 6) * 32 + (cc >> 1) * 16 + (row & 15);
+            img[w * 4 + ((row >> 4) & 3)] = (char)e8[it];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t word = *reinterpret_cast<const uint32_t*>(img + lane * 4);
+    const int nb = n0 + wn * 64;
+    const int R = m0 + wm * 128 + (lane >> 5) * 64;   // brick row base
+    if (nb < N && R < o8.lds)
+        reinterpret_cast<uint32_t*>(o8.s)[(int64_t)(nb >> 7) * o8.lds + R + (((nb >> 5) & 3) + ((lane >> 4) & 1)) * 16 +
+                                          (lane & 15)] = word;
+}
+
+// Pipelined form of store_wave_tile_q8 (same bits): row group i's LN / GELU math and image rows, then that group's
+// quantise + 16-B element stores, so the stores start after the first 16 rows instead of after all 128 and drain
+// under the remaining math (store_wave_tile_pipe's order, for the fp8-only output).
+template <int EPI>
+__device__ __forceinline__ void store_wave_tile_q8_pipe(char* img, const char* aux, const f32x4 (&acc)[4][8], int wm,
+                                                        int wn, int m0, int n0, int lane, int M, int N, Out8 o8) {
+    constexpr bool LN = (EPI == VPF_EPI_LN || EPI == VPF_EPI_LN_GELU);
+    const int fr = lane & 15, fq = lane >> 4, cc = lane & 3;
+    float4 bv[4], cv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = (wn * 64 + j * 16 + fq * 4) * 4;
+        bv[j] = *reinterpret_cast<const float4*>(aux + c);
+        if constexpr (LN) cv[j] = *reinterpret_cast<const float4*>(aux + 1024 + c);
+    }
+    uint32_t e8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        f32x2 rsx = {1.f, 1.f}, rsy = {0.f, 0.f};
+        if constexpr (LN) {
+            const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + (wm * 128 + i * 16 + fr) * 8);
+            rsx = f32x2{st.y, st.y};
+            rsy = f32x2{-st.y * st.x, -st.y * st.x};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f32x2 v01, v23;
+            const f32x2 a01 = {acc[j][i][0], acc[j][i][1]}, a23 = {acc[j][i][2], acc[j][i][3]};
+            const f32x2 b01 = {bv[j].x, bv[j].y}, b23 = {bv[j].z, bv[j].w};
+            if constexpr (LN) {
+                const f32x2 c01 = {cv[j].x, cv[j].y}, c23 = {cv[j].z, cv[j].w};
+                v01 = __builtin_elementwise_fma(rsx, a01, __builtin_elementwise_fma(rsy, c01, b01));
+                v23 = __builtin_elementwise_fma(rsx, a23, __builtin_elementwise_fma(rsy, c23, b23));
+            } else {
+                v01 = a01 + b01;
+                v23 = a23 + b23;
+            }
+            if constexpr (EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU) {
+                v01 = gelu_sig2(v01);
+                v23 = gelu_sig2(v23);
+            }
+            const int row = i * 16 + fr;
+            const int c8 = (j * 4 + fq) ^ (row & 15);
+            *reinterpret_cast<uint2*>(img + row * 128 + c8 * 8) = make_uint2(pack_bf2(v01.x, v01.y), pack_bf2(v23.x, v23.y));
+        }
+        __builtin_amdgcn_wave_barrier();   // the image is private to this wave: its LDS ops stay in order
+        const int row = i * 16 + (lane >> 2);
+        uint4 h[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c16 = 2 * cc + u;
+            uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + ((c16 ^ ((row & 15) >> 1)) * 16));
+            if (row & 1) { const uint32_t t0 = v.x, t1 = v.y; v.x = v.z; v.y = v.w; v.z = t0; v.w = t1; }
+            h[u] = v;
+        }
+        uint32_t am = max(mx8_amax8(h[0]), mx8_amax8(h[1]));
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0xB1, 0xF, 0xF, false));   // lane pair = block
+        const int E = mx8_block_exp(am);
+        e8[i] = (uint32_t)(E + 127);
+        const uint2 q0 = mx8_pack8(h[0], E), q1 = mx8_pack8(h[1], E);
+        const int m = m0 + wm * 128 + row;
+        const int n = n0 + wn * 64 + cc * 16;
+        if (m < M && n < N) *reinterpret_cast<uint4*>(o8.q + (int64_t)m * o8.ldq + n) = make_uint4(q0.x, q0.y, q1.x, q1.y);
+    }
     __builtin_amdgcn_wave_barrier();
     if ((lane & 1) == 0) {
 #pragma unroll

@@ -17,6 +17,7 @@
 // epilogue operands (bias | colsum | up to MX_PARTS statistics planes) = 160 KiB.
 // Epilogues: gemm_common.h store_wave_tile (bias / LN fold / GELU / residual, statistics planes, optional
 // MX-fp8 copy of the output).
+#include <stdlib.h>
 #include "gemm_common.h"
 
 using namespace vpf;
@@ -44,7 +45,19 @@ __device__ __forceinline__ void mx_col(f32x4 (&acc)[8], const i32x8& b, const i3
     VPF_MX(4, sa1); VPF_MX(5, sa1); VPF_MX(6, sa1); VPF_MX(7, sa1);
 }
 #undef VPF_MX
-template <int EPI, bool OUT8>
+// One activation fragment I against the wave's 4 W fragments (the row-major order of the LAB 4 schedule)
+#define VPF_MXR(J) \
+    acc[J][I] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b[J], a, acc[J][I], 0, 0, J, sb, (I) & 3, sa)
+template <int I>
+__device__ __forceinline__ void mx_row(f32x4 (&acc)[4][8], const i32x8 (&b)[4], const i32x8& a, int sb, int sa) {
+    VPF_MXR(0); VPF_MXR(1); VPF_MXR(2); VPF_MXR(3);
+}
+#undef VPF_MXR
+
+// LAB (lab builds only, VPF_MX8_VARIANT 7 / 8 / 9): 1 = no epilogue (the K loop alone), 2 = the loop's DMAs and
+// barriers only, 3 = DMAs + fragment reads (no MFMAs): timing probes that do not write C. 4 (VPF_MX8_VARIANT=6) =
+// the row-major counted-wait schedule, full kernel.
+template <int EPI, bool OUT8, bool EARLY = true, int LAB = 0>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict__ A, int lda,
                                                        const uint32_t* __restrict__ As, int lds_a,
                                                        const uint8_t* __restrict__ W,
@@ -149,6 +162,72 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
         // halves), and the scale of K-block b = [32b, 32b+32) comes from lane group b. So a lane reads logical
         // chunks fq and 4+fq of its row, and supplies the scale of block fq: one word per 64-row brick, byte f
         // = fragment f of the brick (mx8_scale_byte).
+        if constexpr (LAB == 2) {
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            stage(kt & 1, min(kt + 2, nk - 1));
+            continue;
+        }
+        if constexpr (LAB == 4) {
+            // row-major schedule: the W fragments and scale words are read first, then the activation fragments in
+            // row order; row i's 4 MFMAs wait only for its own two reads (counted lgkmcnt), so the MFMAs start after
+            // 13 of the 27 reads instead of all of them. The buffer-release barrier follows row 3, once every read
+            // has landed; the refill's 9 DMA issues go between rows 4-7's MFMAs. Per accumulator the MFMA order
+            // over K-tiles is unchanged: bit-identical to the column schedule.
+            i32x4 bl[4], bh[4], al[8], ah[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = wn * 64 + j * 16 + fr;
+                const int sw = (row >> 1) & 7;
+                bl[j] = lds16(lb + row * 128 + (fq ^ sw) * 16);
+                bh[j] = lds16(lb + row * 128 + ((4 + fq) ^ sw) * 16);
+            }
+            int sb = lds4(lbs + wn * 64 + fq * 16 + fr);
+            int sa0 = lds4(las + (2 * wm) * 64 + fq * 16 + fr);
+            int sa1 = lds4(las + (2 * wm + 1) * 64 + fq * 16 + fr);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = wm * 128 + i * 16 + fr;
+                const int sw = (row >> 1) & 7;
+                al[i] = lds16(la + row * 128 + (fq ^ sw) * 16);
+                ah[i] = lds16(la + row * 128 + ((4 + fq) ^ sw) * 16);
+            }
+            asm volatile("s_waitcnt lgkmcnt(14)"
+                         : "+v"(bl[0]), "+v"(bl[1]), "+v"(bl[2]), "+v"(bl[3]), "+v"(bh[0]), "+v"(bh[1]), "+v"(bh[2]),
+                           "+v"(bh[3]), "+v"(sb), "+v"(sa0), "+v"(sa1), "+v"(al[0]), "+v"(ah[0])
+                         :: "memory");
+            i32x8 b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                b[j] = i32x8{bl[j].x, bl[j].y, bl[j].z, bl[j].w, bh[j].x, bh[j].y, bh[j].z, bh[j].w};
+            auto afr = [&](int i) { return i32x8{al[i].x, al[i].y, al[i].z, al[i].w, ah[i].x, ah[i].y, ah[i].z, ah[i].w}; };
+            mx_row<0>(acc, b, afr(0), sb, sa0);
+            asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(al[1]), "+v"(ah[1]) :: "memory");
+            mx_row<1>(acc, b, afr(1), sb, sa0);
+            asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(al[2]), "+v"(ah[2]) :: "memory");
+            mx_row<2>(acc, b, afr(2), sb, sa0);
+            asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(al[3]), "+v"(ah[3]) :: "memory");
+            mx_row<3>(acc, b, afr(3), sb, sa0);
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(al[4]), "+v"(ah[4]), "+v"(al[5]), "+v"(ah[5]), "+v"(al[6]), "+v"(ah[6]), "+v"(al[7]),
+                           "+v"(ah[7])
+                         :: "memory");
+            __builtin_amdgcn_s_barrier();   // every wave holds K-tile kt in registers: its buffer is free
+            asm volatile("" ::: "memory");
+            stage(kt & 1, min(kt + 2, nk - 1));
+            mx_row<4>(acc, b, afr(4), sb, sa1);
+            mx_row<5>(acc, b, afr(5), sb, sa1);
+            mx_row<6>(acc, b, afr(6), sb, sa1);
+            mx_row<7>(acc, b, afr(7), sb, sa1);
+#pragma unroll
+            for (int q = 0; q < 7; ++q) {   // one DMA issue after every 2 MFMAs, the last two at the end
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+            continue;
+        }
         i32x4 bl[4], bh[4], al[8], ah[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -176,6 +255,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
                      : "+v"(al[0]), "+v"(al[1]), "+v"(al[2]), "+v"(al[3]), "+v"(al[4]), "+v"(al[5]), "+v"(al[6]),
                        "+v"(al[7]), "+v"(ah[0]), "+v"(ah[1]), "+v"(ah[2]), "+v"(ah[3]), "+v"(ah[4]), "+v"(ah[5]),
                        "+v"(ah[6]), "+v"(ah[7]));
+        if constexpr (LAB == 3) {
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            stage(kt & 1, min(kt + 2, nk - 1));
+            continue;
+        }
         i32x8 a[8], b[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -183,24 +268,47 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             a[i] = i32x8{al[i].x, al[i].y, al[i].z, al[i].w, ah[i].x, ah[i].y, ah[i].z, ah[i].w};
-        // the first column group's 8 MFMAs run before the buffer-release barrier (they need only registers), so the
-        // MFMA pipe works while the slower waves finish their reads
-        mx_col<0>(acc[0], b[0], a, sb, sa0, sa1);
+        if constexpr (EARLY) {
+            // the first column group's 8 MFMAs run before the buffer-release barrier (they need only registers),
+            // so the MFMA pipe works while the slower waves finish their reads
+            mx_col<0>(acc[0], b[0], a, sb, sa0, sa1);
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            stage(kt & 1, min(kt + 2, nk - 1));
+            mx_col<1>(acc[1], b[1], a, sb, sa0, sa1);
+            mx_col<2>(acc[2], b[2], a, sb, sa0, sa1);
+            mx_col<3>(acc[3], b[3], a, sb, sa0, sa1);
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {   // one DMA issue after every 2 MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            continue;
+        }
         __builtin_amdgcn_s_barrier();   // every wave holds K-tile kt in registers: its buffer is free
         asm volatile("" ::: "memory");
         stage(kt & 1, min(kt + 2, nk - 1));
         // swapped operands as in the bf16 kernel: W fragment as MFMA-A, activation as MFMA-B -> D[n][m]
+        mx_col<0>(acc[0], b[0], a, sb, sa0, sa1);
         mx_col<1>(acc[1], b[1], a, sb, sa0, sa1);
         mx_col<2>(acc[2], b[2], a, sb, sa0, sa1);
         mx_col<3>(acc[3], b[3], a, sb, sa0, sa1);
 #pragma unroll
-        for (int q = 0; q < 9; ++q) {   // one DMA issue after every 2 MFMAs
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        for (int q = 0; q < 9; ++q) {   // one DMA issue after every 3 MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
             __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing refills land before the ring is reused
+    if constexpr (LAB >= 1 && LAB <= 3) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(acc[j][i]));
+        return;
+    }
 
     if constexpr (LN) {
         if (stats_parts > 0 && tid < BM) {   // planes -> {mean, rstd} once per row (see gemm_bf16.hip)
@@ -227,7 +335,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
     float* prod_stats = EPI == VPF_EPI_BIAS_RESIDUAL ? stats_out : nullptr;
     char* img = smem + wid * 16384;
     if (OUT8 && C == nullptr) {   // fp8-only output (FC1): 16-B element stores, gathered scale words
-        store_wave_tile_q8<EPI>(img, aux, acc, wm, wn, m0, n0, lane, M, N, o8);
+        if constexpr (LAB == 5) store_wave_tile_q8_pipe<EPI>(img, aux, acc, wm, wn, m0, n0, lane, M, N, o8);
+        else store_wave_tile_q8<EPI>(img, aux, acc, wm, wn, m0, n0, lane, M, N, o8);
+        return;
+    }
+    if constexpr (LAB == 5 && !OUT8 && EPI != VPF_EPI_BIAS_RESIDUAL) {   // bf16 output only (QKV): the pipelined pass
+        store_wave_tile_pipe<EPI>(img, aux, acc, wm, wn, m0, n0, lane, res, C, ldc, M, N, nullptr, 0);
         return;
     }
     store_wave_tile<EPI, OUT8>(img, aux, acc, wm, wn, m0, n0, lane, res, nullptr, 1, C, ldc, M, N, prod_stats, M, o8);
@@ -259,10 +372,27 @@ __global__ __launch_bounds__(256) void k_quantize_mx8(const bf16_t* __restrict__
 #define VPF_MX8_ARGS                                                                                         \
     A, (int)lda, As, (int)lds_a, W, Ws, bias, residual, reinterpret_cast<const float2*>(row_stats), colsum,    \
         C, (int)ldc, (int)M, (int)N, (int)K, group, stats_parts, ln_eps, stats_out, o8
+#ifdef VPF_GEMM_LAB
+#define VPF_MX8_LAB_LAUNCH(E)                                                                                \
+        if (labv == 1) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 1>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 2) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 2>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 3) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 3>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 4 && o8.q) { hipLaunchKernelGGL((k_gemm_mx8<E, true, true, 4>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 4) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 4>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 5 && o8.q) { hipLaunchKernelGGL((k_gemm_mx8<E, true, true, 5>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 5) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 5>), grid, block, 0, s, VPF_MX8_ARGS); break; }
+#else
+#define VPF_MX8_LAB_LAUNCH(E)
+#endif
 #define VPF_MX8_LAUNCH(E)                                                                                    \
     do {                                                                                                     \
-        if (o8.q)                                                                                            \
+        VPF_MX8_LAB_LAUNCH(E)                                                                                \
+        if (o8.q && late)                                                                                    \
+            hipLaunchKernelGGL((k_gemm_mx8<E, true, false>), grid, block, 0, s, VPF_MX8_ARGS);                \
+        else if (o8.q)                                                                                       \
             hipLaunchKernelGGL((k_gemm_mx8<E, true>), grid, block, 0, s, VPF_MX8_ARGS);                       \
+        else if (late)                                                                                       \
+            hipLaunchKernelGGL((k_gemm_mx8<E, false, false>), grid, block, 0, s, VPF_MX8_ARGS);               \
         else                                                                                                 \
             hipLaunchKernelGGL((k_gemm_mx8<E, false>), grid, block, 0, s, VPF_MX8_ARGS);                      \
     } while (0)
@@ -292,6 +422,13 @@ VPF_API int vpf_gemm_mx8(const uint8_t* A, int64_t lda, const uint32_t* As, int6
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)tiles), block(NTHREADS);
     const int group = vpf_gemm_tile_group_mx8(epilogue);
+    // VPF_MX8_VARIANT=0: the previous schedule (all MFMAs after the buffer-release barrier), for A/B timing
+    const char* var = getenv("VPF_MX8_VARIANT");
+    const bool late = var && var[0] == '0';
+    // lab builds: 7 / 8 / 9 -> LAB 1 / 2 / 3 (probes), 6 -> LAB 4 (row-major schedule, full kernel)
+    const int labv = var && var[0] >= '7' && var[0] <= '9' ? var[0] - '6' : var && var[0] == '6' ? 4
+                     : var && var[0] == '5' ? 5 : 0;   // 5 -> LAB 5: the pipelined fp8-only epilogue
+    (void)labv;
     switch (epilogue) {
         case VPF_EPI_BIAS: VPF_MX8_LAUNCH(VPF_EPI_BIAS); break;
         case VPF_EPI_BIAS_GELU: VPF_MX8_LAUNCH(VPF_EPI_BIAS_GELU); break;

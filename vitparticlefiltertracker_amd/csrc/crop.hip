@@ -100,74 +100,14 @@ __global__ __launch_bounds__(256) void k_crop_patches(const uint32_t* __restrict
     }
 }
 
-// Fast path (patch % 8 == 0, Kp == 3 patch^2): one thread = 8 consecutive output pixels of one patch row
-// (ky, kx0..kx0+7) in all three channels. The source row (sy, fy, iy) is computed once, each sample's
-// column once, and one dword tap serves all three channels: 32 loads for 24 outputs instead of 96.
-// Same per-value arithmetic (and order) as the generic kernel and the oracle.
-template <typename OutT>
-__global__ __launch_bounds__(256) void k_crop_patches_fast(const uint32_t* __restrict__ rgba, int H, int W,
-                                                           const float* __restrict__ xs,
-                                                           const float* __restrict__ ys,
-                                                           const float* __restrict__ ss, int64_t n_rows,
-                                                           int n_patches, int g, float w0, float h0, int S,
-                                                           int patch, NormAB nab, OutT* __restrict__ out) {
-    const int per_row = patch * (patch >> 3);             // threads per im2col row
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid >= n_rows * per_row) return;
-    const int64_t row = tid / per_row;
-    const int t = (int)(tid - row * per_row);
-    const int ky = t / (patch >> 3), kx0 = (t - ky * (patch >> 3)) * 8;
-    const int64_t p = row / n_patches;
-    const int pi = (int)(row - p * n_patches);
-    const int py = pi / g, px = pi - (pi / g) * g;
-    const float s = ss[p];
-    const float bw = s * w0, bh = s * h0;
-    const float x0 = xs[p] - 0.5f * bw, y0 = ys[p] - 0.5f * bh;
-    const float dx = bw / (float)S, dy = bh / (float)S;
-    const int oy = py * patch + ky;
-    const float sy = (y0 + ((float)oy + 0.5f) * dy) - 0.5f;
-    const float fy0 = floorf(sy);
-    const float fy = sy - fy0;
-    const int iy = (int)fy0;
-    float vals[3][8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int ox = px * patch + kx0 + e;
-        const float sx = (x0 + ((float)ox + 0.5f) * dx) - 0.5f;
-        const float fx0 = floorf(sx);
-        const float fx = sx - fx0;
-        const int ix = (int)fx0;
-        const uint32_t t00 = rgba_tap(rgba, H, W, iy, ix), t01 = rgba_tap(rgba, H, W, iy, ix + 1);
-        const uint32_t t10 = rgba_tap(rgba, H, W, iy + 1, ix), t11 = rgba_tap(rgba, H, W, iy + 1, ix + 1);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float top = (1.0f - fx) * chan(t00, c) + fx * chan(t01, c);
-            const float bot = (1.0f - fx) * chan(t10, c) + fx * chan(t11, c);
-            const float v = (1.0f - fy) * top + fy * bot;
-            vals[c][e] = fmaf(v, nab.a[c], nab.b[c]);
-        }
-    }
-    const int pp = patch * patch;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        OutT* dst = out + row * (int64_t)(3 * pp) + c * pp + ky * patch + kx0;
-        if constexpr (sizeof(OutT) == 2) {
-            uint4 pk;
-            pk.x = pack_bf2(vals[c][0], vals[c][1]); pk.y = pack_bf2(vals[c][2], vals[c][3]);
-            pk.z = pack_bf2(vals[c][4], vals[c][5]); pk.w = pack_bf2(vals[c][6], vals[c][7]);
-            *reinterpret_cast<uint4*>(dst) = pk;
-        } else {
-            *reinterpret_cast<float4*>(dst) = make_float4(vals[c][0], vals[c][1], vals[c][2], vals[c][3]);
-            *reinterpret_cast<float4*>(dst + 4) = make_float4(vals[c][4], vals[c][5], vals[c][6], vals[c][7]);
-        }
-    }
-}
-
-// LDS-staged form of the fast path: one 512-thread workgroup per particle. The particle's source window (every
+// Fast path (patch % 8 == 0, Kp == 3 patch^2), LDS-staged: one 512-thread workgroup per particle; a thread writes 8
+// consecutive output pixels of one patch row (ky, kx0..kx0+7) in all three channels, the source row (sy, fy, iy)
+// computed once, each sample's column once, and one dword tap serving all three channels. The particle's source window (every The particle's source window (every
 // bilinear tap of its S x S samples, clamped into the zero border as rgba_tap does) is copied from the RGBA workspace
 // into LDS once, and the taps read LDS instead of issuing 32 gathered dword loads per thread through the vector
 // memory path, which bound the global form (the im2col stores are the same). A window larger than CROP_LDS_DW dwords
-// (a large template at a large scale) takes the global taps. Same values and arithmetic as k_crop_patches_fast.
+// (a large template at a large scale) takes the global taps. Same per-value arithmetic (and order) as the generic
+// kernel and the oracle.
 #ifndef VPF_CROP_LDS_DW
 #define VPF_CROP_LDS_DW 10240   // -DVPF_CROP_LDS_DW=n builds A/B variants (tools/ab_libs.sh)
 #endif
@@ -268,17 +208,9 @@ static int crop_launch(const uint8_t* frame, int H, int W, uint32_t* rgba_ws, co
     hipLaunchKernelGGL(k_frame_rgba, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, frame, H, W, rgba_ws);
     const int g = S / patch;
     const int64_t rows = n * g * g;
-    // VPF_CROP_LDS=0: the global-tap kernel for the fast path (A/B timing)
-    const char* lds_env = getenv("VPF_CROP_LDS");
-    const bool use_lds = !(lds_env && lds_env[0] == '0');
-    if (patch % 8 == 0 && Kp == 3 * patch * patch && use_lds && n <= INT32_MAX) {
+    if (patch % 8 == 0 && Kp == 3 * patch * patch && n <= INT32_MAX) {
         hipLaunchKernelGGL(k_crop_patches_lds<OutT>, dim3((unsigned)n), dim3(512), 0, st, rgba_ws, H, W, particles,
                            particles + ld, particles + 2 * ld, g * g, g, w0, h0, S, patch, nab, out);
-    } else if (patch % 8 == 0 && Kp == 3 * patch * patch) {
-        const int64_t work = rows * (patch * (patch / 8));
-        hipLaunchKernelGGL(k_crop_patches_fast<OutT>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, rgba_ws,
-                           H, W, particles, particles + ld, particles + 2 * ld, rows, g * g, g, w0, h0, S, patch, nab,
-                           out);
     } else {
         const int64_t work = rows * (Kp / 8);
         hipLaunchKernelGGL(k_crop_patches<OutT>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, rgba_ws, H, W,

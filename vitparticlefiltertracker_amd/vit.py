@@ -28,7 +28,6 @@ for N > 256, the attention output and proj).
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, Optional
 
 import torch
@@ -95,7 +94,10 @@ def _run(timer, name, fn, *args):
 
 class ViTEngine:
     def __init__(self, arch: ViTArch, weights: Dict[str, torch.Tensor], dtype: str, device, batch: int,
-                 mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5)):
+                 mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5), cls_fused: bool = True, cls_splitk: bool = True):
+        """`cls_fused` / `cls_splitk` (default on, the product): the last block's folded CLS attention and its split-K
+        CLS-row fc2. Off selects the K / V GEMM + attention path and the one-pass fc2 they replace (tests, A/B); no
+        environment variable changes what the engine runs."""
         if not torch.cuda.is_available():
             raise _lib.VPFError("ViTEngine needs a HIP device (the product path has no CPU fallback)")
         _lib.lib()  # fail loudly now if libvpf.so is missing
@@ -177,10 +179,10 @@ class ViTEngine:
         #   G[p][h D + i] = sum_{k in head h} q[p][k] W'_k[k][i]   block-diagonal GEMM (W_G[h D + i][k] = W'_k[k][i])
         #   x[p][64 h + d] = sum_i W'_v[64 h + d][i] U[p][h D + i] + b'_v[64 h + d]: one dense GEMM of the (p, h)
         #   rows of U against W'_v, then the diagonal blocks gathered (vpf_head_gather_bf16)
-        # VPF_CLS_FUSED=0 keeps the K / V GEMM + attention path (A/B, tests).
+        # cls_fused=False keeps the K / V GEMM + attention path (A/B, tests).
         H = A.heads
-        self.cls_fused = (self.fold_ln and H in (6, 12, 16) and D == 64 * H and N <= 640
-                          and os.environ.get("VPF_CLS_FUSED", "1") != "0")
+        self.cls_fused = bool(cls_fused) and self.fold_ln and H in (6, 12, 16) and D == 64 * H and N <= 640
+        self.cls_splitk = bool(cls_splitk)
         if self.cls_fused:
             L = self.layers[-1]
             Wk = L["wqkv"][D:2 * D].float()
@@ -314,7 +316,7 @@ class ViTEngine:
         P, eps = self.parts, A.ln_eps
         pl = self.planes(n) if planes else None                # planes of h2 (written by embed / proj / fc2)
         ws = self.splitk_ws if fold else None
-        sk = fold and os.environ.get("VPF_CLS_SPLITK", "1") != "0"   # 0: the one-pass kernel (A/B timing)
+        sk = fold and self.cls_splitk                         # False: the one-pass kernel (A/B timing)
 
         def q_cls():
             """The CLS rows' LN-folded query (row statistics from the row_stats pass in stc)."""
