@@ -17,8 +17,9 @@ resident in HBM before the timed region. Rank 0 prints ONE JSON line. Extra fiel
   frame_mfma_frac  whole-frame algorithmic FLOPs (35.126 GFLOP/crop) x fps / peak.
   kernels       per-kernel-type HIP-event averages from the same eager pass.
   cpu_baseline  the CPU oracle (torch fp32 ViT + C particle-filter ops, "port": the reference has no
-                runnable code) timed on this host's cores on a bounded crop sample, extrapolated to one
-                4096-particle frame (rank 0, N = 1 only).
+                runnable code) timed on this host's cores: ONE full tracking frame at the workload's particle count
+                (OracleTracker.track after a warm-up batch; ~160-190 s for 4096 particles on 16 cores), with the
+                bounded crop-sample extrapolation of earlier rounds beside it as a cross-check (rank 0, N = 1 only).
 """
 from __future__ import annotations
 
@@ -36,30 +37,36 @@ PEAK_BF16_TFLOPS = 2500.0     # dense bf16 MFMA, /opt/skills/guides/MI355X_MICRO
 PEAK_FP8_TFLOPS = 5000.0      # dense block-scaled e4m3 MFMA (same table), the fp8 path's GEMMs
 
 
-# newest committed PMC summary first (profiles/r<round>_pmc_traffic[_<dtype>].json)
+# newest committed PMC summary first (profiles/r<round>_pmc_traffic[_<dtype>][_<tag>].json)
 def _pmc_files(dtype: str):
+    import glob
+    import re
     suffix = "" if dtype == "bf16" else f"_{dtype}"
-    return [os.path.join(ROOT, "profiles", f"r{r}_pmc_traffic{suffix}.json") for r in (3, 2, 1)]
+    out = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_traffic{suffix}*.json")):
+        m = re.match(rf"r(\d+)_pmc_traffic{suffix}(_[a-z0-9]+)?\.json$", os.path.basename(path))
+        if m and (dtype != "bf16" or not (m.group(2) or "").startswith("_fp")):
+            out.append((int(m.group(1)), path))
+    return [p for _, p in sorted(out, reverse=True)]
 
 
-def pmc_traffic(arch_name: str, n_local: int, kernel: str, dtype: str = "bf16"):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_traffic.py over two
-    rocprofv3 passes of this bench: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when it was taken on the
-    same workload; otherwise (None, reason)."""
+def pmc_traffic(arch_name: str, n_local: int, kernel: str, dtype: str = "bf16", frame=None):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (tools/pmc_traffic.py over two rocprofv3
+    passes of this bench: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) taken on the same workload (arch, particles
+    per GPU, dtype, and the source frame when the summary records it); otherwise (None, reason)."""
     for path in _pmc_files(dtype):
-        if not os.path.exists(path):
-            continue
         try:
             with open(path) as f:
                 d = json.load(f)
             if (d.get("arch") != arch_name or int(d.get("particles_per_gpu", -1)) != n_local
-                    or d.get("dtype", "bf16") != dtype):
-                return None, "no PMC summary for this workload"
+                    or d.get("dtype", "bf16") != dtype
+                    or (frame is not None and d.get("frame") not in (None, list(frame)))):
+                continue
             k = d["kernels"][kernel]
             return int(k["traffic_bytes"]), os.path.relpath(path, ROOT)
         except (OSError, KeyError, ValueError):
-            return None, "no PMC summary"
-    return None, "no PMC summary"
+            continue
+    return None, "no PMC summary for this workload"
 
 
 # BASELINE.json configs as presets (global particle count, arch, dtype, frame). configs[0] is the reference's
@@ -92,9 +99,13 @@ def parse():
                     help="collective backend for N > 1: nccl (= RCCL over xGMI, the product path) or gloo "
                          "(host-staged; lets several ranks share one GPU to rehearse the multi-rank path)")
     ap.add_argument("--kernel-frames", type=int, default=2, help="eager frames timed per kernel (roofline)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (s); 0 = skip")
+    ap.add_argument("--cpu-baseline", default="full", choices=["full", "sample", "off"],
+                    help="full: time one whole oracle frame (value) + the bounded sample (cross-check); sample: the "
+                         "bounded-sample extrapolation only; off: skip")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded-sample budget (s); 0 = no sample")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="0 = every core this process may use (affinity, capped by a cgroup quota / OMP_NUM_THREADS)")
+                    help="0 = host_cpus() rule: the affinity set, capped by a cgroup quota and OMP_NUM_THREADS, and "
+                         "at 16 when neither is set")
     args = ap.parse_args()
     if args.preset is not None:
         given = {a.lstrip("-").split("=")[0].replace("-", "_") for a in sys.argv[1:] if a.startswith("--")}
@@ -104,9 +115,13 @@ def parse():
     return args
 
 
+CPU_THREAD_CAP = 16   # the GPU box's CPU share per GPU (cgroup quota 16, OMP_NUM_THREADS=16): the rounds-1-2 default
+
+
 def host_cpus():
     """The host's CPU model and the cores this process may use: its affinity set, capped by a cgroup CPU quota
-    and by OMP_NUM_THREADS when the launcher sets one (the GPU box's CPU share: it sets 16 per GPU)."""
+    and by OMP_NUM_THREADS when the launcher sets one (the GPU box's CPU share: it sets 16 per GPU); with neither,
+    capped at CPU_THREAD_CAP so the baseline's thread count is the same on every host."""
     info = {"affinity": len(os.sched_getaffinity(0)), "cgroup_quota": None, "omp_num_threads": None, "model": None}
     try:
         with open("/proc/cpuinfo") as f:
@@ -130,7 +145,11 @@ def host_cpus():
         use = min(use, max(1, int(info["cgroup_quota"])))
     if info["omp_num_threads"]:
         use = min(use, info["omp_num_threads"])
+    if not info["cgroup_quota"] and not info["omp_num_threads"]:
+        use = min(use, CPU_THREAD_CAP)
     info["threads"] = use
+    info["thread_rule"] = (f"min(affinity, cgroup quota, OMP_NUM_THREADS); {CPU_THREAD_CAP} when neither quota nor "
+                           "OMP_NUM_THREADS is set")
     return info
 
 
@@ -185,7 +204,8 @@ def cpu_baseline(arch_name: str, P: int, budget_s: float, threads: int):
     t_pf = time.perf_counter() - t1
     s_per_frame = t_vit * P + t_pf
     return {"value": 1.0 / s_per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
-            "cpu_model": cpus["model"], "host_cpus": {k: cpus[k] for k in ("affinity", "cgroup_quota", "omp_num_threads")},
+            "cpu_model": cpus["model"],
+            "host_cpus": {k: cpus[k] for k in ("affinity", "cgroup_quota", "omp_num_threads", "thread_rule")},
             "s_per_frame": round(s_per_frame, 2), "s_per_crop": round(t_vit, 5),
             "s_per_crop_mean": round(t_vit_mean, 5), "pf_ops_s": round(t_pf, 5),
             "extrapolation": f"s/frame = median s/crop (per batch of {batch}) x {P} crops + PF ops at P={P} (linear in "
@@ -194,6 +214,62 @@ def cpu_baseline(arch_name: str, P: int, budget_s: float, threads: int):
             "sample": f"{crops} crops of {arch_name} fp32 (torch CPU oracle, batch {batch}) in "
                       f"{t_vit * crops:.1f} s + PF ops at P={P}; extrapolated to one {P}-particle frame "
                       f"({s_per_frame:.1f} s/frame)"}
+
+
+def cpu_full_frame(arch_name: str, P: int, threads: int, sample_s: float):
+    """cpu_baseline: ONE full tracking frame of the CPU oracle at the workload's particle
+    count, measured: OracleTracker.init on frame 0, a warm-up batch, then OracleTracker.track on frame 1 (predict, P
+    crops through the fp32 ViT in batches of 8, weights, estimate, resample), wall clock. Progress to stderr every 512
+    crops. With sample_s > 0 the bounded-sample extrapolation (cpu_baseline above) runs after it as a cross-check."""
+    import numpy as np
+    import torch
+
+    from oracle.tracker import OracleTracker
+    from vitparticlefiltertracker_amd.config import ARCHS, load_config
+    from vitparticlefiltertracker_amd.frames import synthetic_clip
+    from vitparticlefiltertracker_amd.weights import make_vit_weights
+
+    arch = ARCHS[arch_name]
+    cpus = host_cpus()
+    threads = threads or cpus["threads"]
+    torch.set_num_threads(threads)
+    cfg = load_config({"model": {"arch": arch_name, "dtype": "fp32"}, "particles": {"num": P}})
+    w = make_vit_weights(arch, seed=int(cfg["model"]["weights"]["seed"]))
+    clip = synthetic_clip(2)
+    ot = OracleTracker(cfg, w, arch)
+    ot.init(clip[0], cfg["input"]["bbox0"])
+    ot.features(clip[1], np.ascontiguousarray(ot.particles[:, :8]), 8)        # warm-up batch
+    feats, done, t0 = ot.features, [0], [0.0]
+
+    def features_with_progress(frame, particles, chunk=None):
+        out = []
+        for i in range(0, particles.shape[1], 512):
+            out.append(feats(frame, np.ascontiguousarray(particles[:, i:i + 512]), 8))
+            done[0] += out[-1].shape[0]
+            print(f"bench.py cpu_baseline: {done[0]} / {particles.shape[1]} crops, {time.perf_counter() - t0[0]:.1f} s",
+                  file=sys.stderr, flush=True)
+        return np.concatenate(out, 0)
+
+    ot.features = features_with_progress
+    t0[0] = time.perf_counter()
+    ot.track(clip[1])
+    measured = time.perf_counter() - t0[0]
+    out = {"value": 1.0 / measured, "unit": "frames/s", "cores": threads, "kind": "port",
+           "cpu_model": cpus["model"],
+           "host_cpus": {k: cpus[k] for k in ("affinity", "cgroup_quota", "omp_num_threads", "thread_rule")},
+           "s_per_frame": round(measured, 2), "measured": "full frame",
+           "sample": f"one full {P}-particle tracking frame of the CPU oracle (OracleTracker.track: predict, {P} crops "
+                     f"of {arch_name} fp32 through the torch CPU ViT in batches of 8, weights, estimate, resample), "
+                     f"after a warm-up batch: {measured:.1f} s"}
+    if sample_s > 0:
+        try:
+            x = cpu_baseline(arch_name, P, sample_s, threads)
+            out["cross_check"] = {k: x[k] for k in ("s_per_frame", "s_per_crop", "s_per_crop_mean", "pf_ops_s",
+                                                    "sample")}
+            out["cross_check"]["extrapolated_over_measured"] = round(x["s_per_frame"] / measured, 4)
+        except Exception as e:  # report, never fake
+            out["cross_check"] = {"error": repr(e)}
+    return out
 
 
 def main() -> int:
@@ -275,7 +351,7 @@ def main() -> int:
             v["tflops"] = flops[name] / (v["avg_ms"] * 1e-3) / 1e12
     dom = max((n for n in flops if n.startswith("gemm") and n in ks), key=lambda n: ks[n]["total_ms"])
     ach = ks[dom]["tflops"]
-    traffic, traffic_src = (pmc_traffic(args.arch, n_loc, dom, args.dtype) if args.dtype in ("bf16", "fp8")
+    traffic, traffic_src = (pmc_traffic(args.arch, n_loc, dom, args.dtype, (fh, fw)) if args.dtype in ("bf16", "fp8")
                             else (None, None))
     # the dominant GEMM's MFMA peak: dense bf16, or dense MX-fp8 for the fp8 path's block-scaled GEMMs
     peak = PEAK_FP8_TFLOPS if args.dtype == "fp8" and dom in ("gemm_qkv", "gemm_fc1", "gemm_fc2") else PEAK_BF16_TFLOPS
@@ -320,9 +396,12 @@ def main() -> int:
         **({"multi_rank_check": check} if check is not None else {}),
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_baseline != "off":
         try:
-            line["cpu_baseline"] = cpu_baseline(args.arch, args.particles, args.cpu_seconds, args.cpu_threads)
+            if args.cpu_baseline == "full":
+                line["cpu_baseline"] = cpu_full_frame(args.arch, args.particles, args.cpu_threads, args.cpu_seconds)
+            elif args.cpu_seconds > 0:
+                line["cpu_baseline"] = cpu_baseline(args.arch, args.particles, args.cpu_seconds, args.cpu_threads)
         except Exception as e:  # report, never fake
             line["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

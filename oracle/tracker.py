@@ -7,10 +7,14 @@ which is absent).
 
 `track(frame, Q=None)`: when `Q` is given (e.g. the GPU's int64 weights of the same frame) the oracle's own
 likelihood is bypassed — the "feature injection" mode that makes resample parity bit-exact.
+
+SPEC S9 (§8f rank 4): `likelihood.template_update` = alpha updates the template after each frame's estimate from the
+feature at that estimate (`OracleTracker.update_template`); `OracleMultiTracker` runs K targets, each with its own box,
+template and particle seed (seed + k), as independent single-target trackers.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -32,6 +36,7 @@ class OracleTracker:
         self.lam = float(cfg["likelihood"]["lambda"])
         self.bits = int(cfg["likelihood"]["weight_bits"])
         self.mean, self.std = cfg["model"]["mean"], cfg["model"]["std"]
+        self.alpha = float(cfg["likelihood"].get("template_update", 0.0))
         self.particles = None
         self.template = None
         self.frame_index = 0
@@ -79,4 +84,40 @@ class OracleTracker:
         anc = pf.resample(Qr, pf.resample_U(self.seed, self.frame_index))
         self.last_ancestors = anc
         self.particles = np.ascontiguousarray(self.particles[:, anc])
+        if self.alpha > 0.0:
+            self.update_template(frame, est)
         return est
+
+    def update_template(self, frame: np.ndarray, state, alpha: Optional[float] = None) -> None:
+        """SPEC S9: t <- g / |g|, g = (1 - alpha) t + alpha f / |f|, f the feature of the crop at `state` (fp32) with
+        the template box on this frame; fp32 arithmetic."""
+        a = np.float32(self.alpha if alpha is None else alpha)
+        st = np.array([[state[0]], [state[1]], [state[2]]], np.float32)
+        f = self.features(frame, st)[0].astype(np.float32)
+        g = (np.float32(1.0) - a) * self.template + a * (f / np.linalg.norm(f))
+        self.template = (g / np.linalg.norm(g)).astype(np.float32)
+
+
+class OracleMultiTracker:
+    """SPEC S9 multi-object mirror of vitparticlefiltertracker_amd.MultiTracker: target k is an OracleTracker with the
+    particle seed particles.seed + k, initialised on its own box (so it crops with its own template box and weighs
+    against its own template), and template-updated from its own estimate when likelihood.template_update > 0."""
+
+    def __init__(self, cfg: dict, n_objects: int, weights, arch, threads: Optional[int] = None):
+        import copy
+        self.K = int(n_objects)
+        self.targets: List[OracleTracker] = []
+        for k in range(self.K):
+            c = copy.deepcopy(cfg)
+            c["particles"]["seed"] = int(cfg["particles"]["seed"]) + k
+            self.targets.append(OracleTracker(c, weights, arch, threads if k == 0 else None))
+
+    def init(self, frame: np.ndarray, bboxes: Sequence) -> None:
+        if len(bboxes) != self.K:
+            raise ValueError(f"expected {self.K} boxes")
+        for t, b in zip(self.targets, bboxes):
+            t.init(frame, b)
+
+    def track(self, frame: np.ndarray, Qs: Optional[Sequence[np.ndarray]] = None) -> List[Tuple[float, float, float]]:
+        """One frame for every target; `Qs[k]` (optional) injects target k's weights as OracleTracker.track does."""
+        return [t.track(frame, None if Qs is None else Qs[k]) for k, t in enumerate(self.targets)]

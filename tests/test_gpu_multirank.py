@@ -89,17 +89,31 @@ def test_sharded_tracker_equals_single_rank(world, P):
 BOXES = [(40, 50, 48, 48), (120, 100, 56, 40)]
 
 
+def _mt_cfg(P, dtype="bf16", alpha=0.0):
+    from vitparticlefiltertracker_amd import load_config
+    return load_config({"model": {"arch": "vit_tiny_patch16_224", "dtype": dtype, "weights": {"seed": 3}},
+                        "particles": {"num": P, "seed": 99}, "likelihood": {"template_update": alpha}})
+
+
 def _mt_run(mt, clip):
+    """Per frame: every target's estimate, this rank's weights (before the resample), ancestors and states."""
     out = []
     mt.init(clip[0], BOXES)
     for f in clip[1:]:
-        ests = mt.track(f)
+        mt._upload(f)
+        mt.frame_index += 1
+        for pf in mt.pfs:
+            pf.height, pf.width = int(f.shape[0]), int(f.shape[1])
+            pf.predict(mt.frame_index)
+        mt.weigh()
+        Qs = [pf.Q.cpu().numpy().copy() for pf in mt.pfs]
+        ests = mt.step()
         out.append((ests, [pf.last_ancestors.cpu().numpy().copy() for pf in mt.pfs],
-                    [pf.particles.cpu().numpy().copy() for pf in mt.pfs]))
+                    [pf.particles.cpu().numpy().copy() for pf in mt.pfs], Qs))
     return out
 
 
-def _mt_worker(rank, world, port, P, q):
+def _mt_worker(rank, world, port, P, dtype, alpha, q):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -107,7 +121,7 @@ def _mt_worker(rank, world, port, P, q):
     try:
         from vitparticlefiltertracker_amd import MultiTracker
         from vitparticlefiltertracker_amd.frames import synthetic_clip
-        mt = MultiTracker(_cfg(P), n_objects=len(BOXES), device="cuda:0", rank=rank, world_size=world)
+        mt = MultiTracker(_mt_cfg(P, dtype, alpha), n_objects=len(BOXES), device="cuda:0", rank=rank, world_size=world)
         q.put((rank, _mt_run(mt, synthetic_clip(FRAMES + 1))))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, repr(e)))
@@ -116,28 +130,80 @@ def _mt_worker(rank, world, port, P, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,P", [(2, 128), (3, 33)])
-def test_sharded_multitracker_equals_single_rank(world, P):
-    """Two targets, each target's particles sharded over the ranks: every rank returns the single-rank
-    MultiTracker's estimates bit for bit, and its shards of every target's ancestors and states."""
-    from vitparticlefiltertracker_amd import MultiTracker
-    from vitparticlefiltertracker_amd.frames import synthetic_clip
-    ref = _mt_run(MultiTracker(_cfg(P), n_objects=len(BOXES), device="cuda:0"), synthetic_clip(FRAMES + 1))
+def _mt_sharded(world, P, dtype="bf16", alpha=0.0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_mt_worker, args=(r, world, port, P, q)) for r in range(world)]
+    procs = [ctx.Process(target=_mt_worker, args=(r, world, port, P, dtype, alpha, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    n = P // world
     for r in range(world):
         assert not isinstance(out[r], str), out[r]
-        for k, ((ests, ancs, parts), (ests1, ancs1, parts1)) in enumerate(zip(out[r], ref), start=1):
+    return out
+
+
+@pytest.mark.parametrize("world,P,alpha", [(2, 128, 0.0), (3, 33, 0.5)])
+def test_sharded_multitracker_equals_single_rank_and_oracle(world, P, alpha):
+    """Two targets with different boxes, each target's particles sharded over the ranks (bf16):
+    * every rank returns the single-rank MultiTracker's estimates bit for bit, and its shards of every target's
+      weights, ancestors and states;
+    * against the oracle directly: the ranks' weight shards, concatenated in rank order, injected into
+      OracleMultiTracker give every rank's ancestors and states bit for bit and the estimates to 1e-12, every frame.
+    (3, 33): 11 particles per rank per target, odd shard chunks; alpha = 0.5: the template update on every rank."""
+    from oracle.tracker import OracleMultiTracker
+    from vitparticlefiltertracker_amd import MultiTracker
+    from vitparticlefiltertracker_amd.config import ARCHS
+    from vitparticlefiltertracker_amd.frames import synthetic_clip
+    from vitparticlefiltertracker_amd.weights import make_vit_weights
+    cfg = _mt_cfg(P, "bf16", alpha)
+    clip = synthetic_clip(FRAMES + 1)
+    ref = _mt_run(MultiTracker(cfg, n_objects=len(BOXES), device="cuda:0"), clip)
+    out = _mt_sharded(world, P, "bf16", alpha)
+    n = P // world
+    K = len(BOXES)
+    for r in range(world):
+        for k, ((ests, ancs, parts, Qs), (ests1, ancs1, parts1, Qs1)) in enumerate(zip(out[r], ref), start=1):
             assert ests == ests1, f"rank {r} frame {k}: estimates {ests} vs single rank {ests1}"
-            for t in range(len(BOXES)):
+            for t in range(K):
+                assert np.array_equal(Qs[t], Qs1[t][r * n:(r + 1) * n]), f"rank {r} frame {k} target {t}: weights"
                 assert np.array_equal(ancs[t], ancs1[t][r * n:(r + 1) * n]), f"rank {r} frame {k} target {t}"
                 assert np.array_equal(parts[t].view(np.uint32), parts1[t][:, r * n:(r + 1) * n].view(np.uint32))
+    arch = ARCHS["vit_tiny_patch16_224"]
+    om = OracleMultiTracker(cfg, K, make_vit_weights(arch, seed=3), arch)
+    om.init(clip[0], BOXES)
+    for k in range(FRAMES):
+        Qg = [np.concatenate([out[r][k][3][t] for r in range(world)]) for t in range(K)]
+        e_ref = om.track(clip[k + 1], Qg)
+        for r in range(world):
+            for t in range(K):
+                np.testing.assert_allclose(out[r][k][0][t], e_ref[t], rtol=1e-12)
+                assert np.array_equal(out[r][k][1][t], om.targets[t].last_ancestors[r * n:(r + 1) * n]), (r, k, t)
+                assert np.array_equal(out[r][k][2][t].view(np.uint32),
+                                      om.targets[t].particles[:, r * n:(r + 1) * n].view(np.uint32)), (r, k, t)
+
+
+def test_sharded_multitracker_fp32_matches_oracle():
+    """Two ranks, two targets, fp32 parity mode with a template update: every rank's per-target estimates within 1e-4
+    relative of OracleMultiTracker's own (no injection), per frame."""
+    from oracle.tracker import OracleMultiTracker
+    from vitparticlefiltertracker_amd.config import ARCHS
+    from vitparticlefiltertracker_amd.frames import synthetic_clip
+    from vitparticlefiltertracker_amd.weights import make_vit_weights
+    world, P = 2, 64
+    cfg = _mt_cfg(P, "fp32", 0.5)
+    clip = synthetic_clip(FRAMES + 1)
+    out = _mt_sharded(world, P, "fp32", 0.5)
+    arch = ARCHS["vit_tiny_patch16_224"]
+    om = OracleMultiTracker(cfg, len(BOXES), make_vit_weights(arch, seed=3), arch)
+    om.init(clip[0], BOXES)
+    for k in range(FRAMES):
+        e_ref = om.track(clip[k + 1])
+        for r in range(world):
+            assert out[r][k][0] == out[0][k][0]
+            for t in range(len(BOXES)):
+                np.testing.assert_allclose(np.array(out[r][k][0][t]), np.array(e_ref[t]), rtol=1e-4,
+                                           err_msg=f"rank {r} frame {k + 1} target {t}")

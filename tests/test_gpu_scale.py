@@ -13,6 +13,9 @@ positions"), not only at the small sizes of test_gpu_vit_tracker.py.
 * configs[2]'s layout: 16384 particles as 8 ranks of 2048 sharing cuda:0 over gloo (the one-GPU box cannot pair
   RCCL ranks on one device), ViT-B bf16: every rank's estimates, ancestors and states equal the single-rank
   16384-particle Tracker bit for bit, and those equal the oracle's resample with the GPU's weights injected.
+* configs[4]'s layout: 65,536 particles as 8 ranks of 8192, ViT-B/16 fp8, 1080x1920 frames, all
+  sharing cuda:0 over gloo (~22 GB of HBM per rank): the same three-way equality with the single-rank 65,536-particle
+  fp8 Tracker and the oracle, plus sampled features of the single-rank run against the fp32 oracle (cos >= 0.99).
 """
 import os
 import socket
@@ -125,12 +128,23 @@ def test_configs4_share_fp8_1080p_8192_matches_oracle():
                   min_cos=0.99)
 
 
-# ------------------------------------------------------------------------------------------ configs[2] layout
+# ------------------------------------------------------------------------------- configs[2] / configs[4] layouts
 C2_P, C2_WORLD, C2_FRAMES = 16384, 8, 2
+C4_P, C4_WORLD, C4_FRAMES, C4_HW, C4_BBOX = 65536, 8, 2, (1080, 1920), (900, 500, 64, 64)
 
 
 def _c2_cfg():
     return load_config({"model": {"arch": "vit_base_patch16_224", "dtype": "bf16"}, "particles": {"num": C2_P}})
+
+
+def _c4_cfg():
+    return load_config({"model": {"arch": "vit_base_patch16_224", "dtype": "fp8"}, "particles": {"num": C4_P}})
+
+
+def _layout(which):
+    if which == 2:
+        return _c2_cfg(), C2_WORLD, C2_FRAMES, (224, 224), BBOX0
+    return _c4_cfg(), C4_WORLD, C4_FRAMES, C4_HW, C4_BBOX
 
 
 def _free_port() -> int:
@@ -141,29 +155,38 @@ def _free_port() -> int:
     return port
 
 
-def _c2_run(tr, clip):
+def _c2_run(tr, clip, bbox=BBOX0, sample=None):
+    """Per frame: estimate, this rank's weights, ancestors, states (and, with `sample`, the predicted particles and
+    LN'd CLS features of those local rows)."""
     out = []
-    tr.init(clip[0], BBOX0)
+    tr.init(clip[0], bbox)
     for f in clip[1:]:
         tr._upload(f)
         tr.frame_index += 1
         tr.pf.predict(tr.frame_index)
         tr.weigh()
         Q = tr.pf.Q.cpu().numpy().copy()
+        extra = None
+        if sample is not None:
+            pred = tr.pf.particles.cpu().numpy()[:, sample].copy()
+            tr.engine.weights_from_tokens(tr.n_local, tr.template, tr.lam, tr.bits, want_feat=True)
+            assert np.array_equal(tr.engine.Q[:tr.n_local].cpu().numpy(), Q)
+            extra = (pred, tr.engine.feat[:tr.n_local][torch.from_numpy(sample).to(tr.device)].double().cpu())
         est = tr.pf.step()
-        out.append((est, Q, tr.pf.last_ancestors.cpu().numpy().copy(), tr.pf.particles.cpu().numpy().copy()))
+        out.append((est, Q, tr.pf.last_ancestors.cpu().numpy().copy(), tr.pf.particles.cpu().numpy().copy(), extra))
     return out
 
 
-def _c2_worker(rank, port, q):
+def _layout_worker(which, rank, port, q):
     import torch.distributed as dist
+    cfg, world, frames, hw, bbox = _layout(which)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=C2_WORLD)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from vitparticlefiltertracker_amd import Tracker
-        tr = Tracker(_c2_cfg(), device="cuda:0", rank=rank, world_size=C2_WORLD)
-        q.put((rank, _c2_run(tr, synthetic_clip(C2_FRAMES + 1))))
+        tr = Tracker(cfg, device="cuda:0", rank=rank, world_size=world)
+        q.put((rank, _c2_run(tr, synthetic_clip(frames + 1, hw[0], hw[1], bbox0=bbox), bbox)))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, repr(e)))
         raise
@@ -171,42 +194,61 @@ def _c2_worker(rank, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(900)
-def test_configs2_layout_8_ranks_equal_single_rank_and_oracle():
+def _check_layout(which, n_sample=0, min_cos=0.999):
+    """configs[which]'s multi-GPU layout with every rank on cuda:0: the single-rank run of all P particles against the
+    oracle (Q injected; optionally sampled features), then `world` gloo ranks against the single-rank run."""
     from vitparticlefiltertracker_amd import Tracker
-    cfg = _c2_cfg()
-    clip = synthetic_clip(C2_FRAMES + 1)
+    cfg, world, frames, hw, bbox = _layout(which)
+    P = int(cfg["particles"]["num"])
+    arch = ARCHS[cfg["model"]["arch"]]
+    clip = synthetic_clip(frames + 1, hw[0], hw[1], bbox0=bbox)
+    idx = _sample_particles(P, arch.tokens, n_sample, fc1_cols=arch.mlp) if n_sample else None
     tr = Tracker(cfg, device="cuda:0")
-    ref = _c2_run(tr, clip)
+    ref = _c2_run(tr, clip, bbox, idx)
     del tr
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     # the single-rank run against the oracle's resample with the GPU's weights injected
-    arch = ARCHS["vit_base_patch16_224"]
-    ot = OracleTracker(cfg, make_vit_weights(arch, seed=0), arch)
-    ot.init(clip[0], BBOX0)
-    for k, (est, Q, anc, parts) in enumerate(ref, start=1):
+    ot = OracleTracker(cfg, make_vit_weights(arch, seed=int(cfg["model"]["weights"]["seed"])), arch)
+    ot.init(clip[0], bbox)
+    for k, (est, Q, anc, parts, extra) in enumerate(ref, start=1):
+        if extra is not None:
+            pred, feat = extra
+            cos = torch.nn.functional.cosine_similarity(feat, _oracle_features(ot, clip[k], pred), dim=1)
+            assert cos.min().item() > min_cos, (k, cos.min().item())
         e_ref = ot.track(clip[k], Q=Q)
         np.testing.assert_allclose(est, e_ref, rtol=1e-12)
         assert np.array_equal(anc, ot.last_ancestors), f"frame {k}: single-rank ancestors vs oracle"
         assert np.array_equal(parts.view(np.uint32), ot.particles.view(np.uint32))
-    # 8 ranks of 2048 on the same GPU
+        assert Q.sum() > 0
+    # `world` ranks of P / world on the same GPU
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_c2_worker, args=(r, port, q)) for r in range(C2_WORLD)]
+    procs = [ctx.Process(target=_layout_worker, args=(which, r, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=600) for _ in procs)
+    out = dict(q.get(timeout=900) for _ in procs)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    n = C2_P // C2_WORLD
-    for r in range(C2_WORLD):
+    n = P // world
+    for r in range(world):
         assert not isinstance(out[r], str), out[r]
-        for k, ((est, Q, anc, parts), (est1, Q1, anc1, parts1)) in enumerate(zip(out[r], ref), start=1):
+        for k, ((est, Q, anc, parts, _), (est1, Q1, anc1, parts1, _)) in enumerate(zip(out[r], ref), start=1):
             assert np.array_equal(Q, Q1[r * n:(r + 1) * n]), f"rank {r} frame {k}: weights"
             assert est == est1, f"rank {r} frame {k}: estimate {est} vs single rank {est1}"
             assert np.array_equal(anc, anc1[r * n:(r + 1) * n]), f"rank {r} frame {k}: ancestors"
             assert np.array_equal(parts.view(np.uint32), parts1[:, r * n:(r + 1) * n].view(np.uint32)), \
                 f"rank {r} frame {k}: particle states"
+
+
+@pytest.mark.timeout(900)
+def test_configs2_layout_8_ranks_equal_single_rank_and_oracle():
+    _check_layout(2)
+
+
+@pytest.mark.timeout(1200)
+def test_configs4_layout_8_ranks_fp8_1080p_equal_single_rank_and_oracle():
+    """configs[4] end to end: 65,536 particles, ViT-B/16 fp8, 1080x1920, as 8 ranks of 8192 (gloo, one GPU)."""
+    _check_layout(4, n_sample=8, min_cos=0.99)

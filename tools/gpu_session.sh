@@ -40,47 +40,55 @@ for step in "$@"; do
     smoke)
       timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
       ok_or_stop $? smoke; tail -5 $OUT/smoke.log ;;
-    bench)
-      timeout -k 10 900 python bench.py --steps 5 --warmup 2 > $OUT/bench.log 2>&1
+    bench)   # the driver's command (N = 1), with its full-frame cpu_baseline
+      timeout -k 10 900 python bench.py --steps 20 --warmup 5 > $OUT/bench.log 2> $OUT/bench.err
       ok_or_stop $? bench; tail -3 $OUT/bench.log ;;
     bench_l)
-      timeout -k 10 900 python bench.py --arch vit_large_patch14_336 --steps 2 --warmup 1 --cpu-seconds 0 > $OUT/bench_l.log 2>&1
+      timeout -k 10 900 python bench.py --arch vit_large_patch14_336 --steps 2 --warmup 1 --cpu-baseline off > $OUT/bench_l.log 2>&1
       ok_or_stop $? bench_l; tail -1 $OUT/bench_l.log | cut -c1-400 ;;
     bench_np)
-      VPF_GEMM_PERSISTENT=0 timeout -k 10 900 python bench.py --steps 5 --warmup 2 --cpu-seconds 0 > $OUT/bench_np.log 2>&1
+      VPF_GEMM_PERSISTENT=0 timeout -k 10 900 python bench.py --steps 5 --warmup 2 --cpu-baseline off > $OUT/bench_np.log 2>&1
       ok_or_stop $? bench_np; tail -1 $OUT/bench_np.log | cut -c1-400 ;;
     prof)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/prof.log 2>&1
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off > $OUT/prof.log 2>&1
       ok_or_stop $? prof; tail -3 $OUT/prof.log ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc_fetch -o p --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernel-frames 1 --cpu-seconds 0 --no-graph > $OUT/pmc_fetch.log 2>&1
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc_fetch -o p --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc_fetch.log 2>&1
       ok_or_stop $? pmc_fetch
-      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc_write -o p --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernel-frames 1 --cpu-seconds 0 --no-graph > $OUT/pmc_write.log 2>&1
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc_write -o p --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc_write.log 2>&1
       ok_or_stop $? pmc_write
       python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write > $OUT/pmc_traffic.json 2> $OUT/pmc_traffic.err
       ok_or_stop $? pmc_traffic; cat $OUT/pmc_traffic.json | head -40 ;;
     pmc8)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc8_fetch -o p --output-format csv -- python3 bench.py --dtype fp8 --steps 1 --warmup 1 --kernel-frames 1 --cpu-seconds 0 --no-graph > $OUT/pmc8_fetch.log 2>&1
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc8_fetch -o p --output-format csv -- python3 bench.py --dtype fp8 --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc8_fetch.log 2>&1
       ok_or_stop $? pmc8_fetch
-      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc8_write -o p --output-format csv -- python3 bench.py --dtype fp8 --steps 1 --warmup 1 --kernel-frames 1 --cpu-seconds 0 --no-graph > $OUT/pmc8_write.log 2>&1
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc8_write -o p --output-format csv -- python3 bench.py --dtype fp8 --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc8_write.log 2>&1
       ok_or_stop $? pmc8_write
       python tools/pmc_traffic.py $OUT/pmc8_fetch $OUT/pmc8_write --dtype fp8 > $OUT/pmc_traffic_fp8.json 2> $OUT/pmc8_traffic.err
       ok_or_stop $? pmc8_traffic; head -40 $OUT/pmc_traffic_fp8.json ;;
+    pmc8_c4)   # PMC traffic of configs[4]'s per-GPU share (8192 particles, fp8, 1080p)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc8c4_fetch -o p --output-format csv -- python3 bench.py --preset 4 --particles 8192 --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc8c4_fetch.log 2>&1
+      ok_or_stop $? pmc8c4_fetch
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc8c4_write -o p --output-format csv -- python3 bench.py --preset 4 --particles 8192 --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc8c4_write.log 2>&1
+      ok_or_stop $? pmc8c4_write
+      python tools/pmc_traffic.py $OUT/pmc8c4_fetch $OUT/pmc8c4_write --dtype fp8 --particles 8192 --frame 1080x1920 > $OUT/pmc_traffic_fp8_c4.json 2> $OUT/pmc8c4_traffic.err
+      ok_or_stop $? pmc8c4_traffic; head -40 $OUT/pmc_traffic_fp8_c4.json ;;
     bench_c4)   # configs[4]'s per-GPU share: 8192 particles, fp8, 1080p
-      timeout -k 10 900 python bench.py --preset 4 --particles 8192 --steps 5 --warmup 2 --cpu-seconds 0 > $OUT/bench_c4.log 2>&1
+      timeout -k 10 900 python bench.py --preset 4 --particles 8192 --steps 5 --warmup 2 --cpu-baseline off > $OUT/bench_c4.log 2>&1
       ok_or_stop $? bench_c4; tail -1 $OUT/bench_c4.log | cut -c1-400 ;;
     bench_p512)   # the 8-GPU share of the 4096-particle frame
-      timeout -k 10 600 python bench.py --particles 512 --steps 10 --warmup 3 --cpu-seconds 0 > $OUT/bench_p512.log 2>&1
+      timeout -k 10 600 python bench.py --particles 512 --steps 10 --warmup 3 --cpu-baseline off > $OUT/bench_p512.log 2>&1
       ok_or_stop $? bench_p512; tail -1 $OUT/bench_p512.log | cut -c1-400 ;;
     prof_c4)   # rocprofv3 kernel stats of configs[4]'s per-GPU share
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof_c4 -o run --output-format csv -- python3 bench.py --preset 4 --particles 8192 --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/prof_c4.log 2>&1
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof_c4 -o run --output-format csv -- python3 bench.py --preset 4 --particles 8192 --steps 3 --warmup 1 --cpu-baseline off > $OUT/prof_c4.log 2>&1
       ok_or_stop $? prof_c4; tail -1 $OUT/prof_c4.log | cut -c1-300 ;;
     bench8)
-      timeout -k 10 900 python bench.py --dtype fp8 --steps 5 --warmup 2 --cpu-seconds 0 > $OUT/bench8.log 2>&1
+      timeout -k 10 900 python bench.py --dtype fp8 --steps 5 --warmup 2 --cpu-baseline off > $OUT/bench8.log 2>&1
       ok_or_stop $? bench8; tail -1 $OUT/bench8.log | cut -c1-600 ;;
     lab)
       timeout -k 10 600 tools/gemm_lab/gemm_lab 5 "$LAB_SHAPES" "$LAB_VARS" 1 > $OUT/lab.log 2>&1

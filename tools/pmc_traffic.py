@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--arch", default="vit_base_patch16_224")
     ap.add_argument("--particles", type=int, default=4096)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--frame", default="224x224", help="the bench run's source frame HxW (recorded for the lookup)")
     a = ap.parse_args()
     from vitparticlefiltertracker_amd.config import ARCHS
     arch = ARCHS[a.arch]
@@ -89,6 +90,7 @@ def main():
                     "gemm_patch": alg["gemm_patch"] + M * D * q})
         alg = {k: int(v) for k, v in alg.items()}
     res = {"arch": a.arch, "particles_per_gpu": a.particles, "dtype": a.dtype,
+           "frame": [int(v) for v in a.frame.lower().split("x")],
            "note": "fetch = 2 x FETCH_SIZE (gfx950 wide-read correction), write = WRITE_SIZE; KiB -> bytes; "
                    "memory-side L2 requests (Infinity-Cache hits included)", "kernels": {}}
     for n, v in sorted(acc.items()):

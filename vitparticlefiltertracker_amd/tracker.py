@@ -26,6 +26,12 @@ from .vit import ViTEngine
 from .weights import make_vit_weights
 
 
+def _blend_template(t: torch.Tensor, f: torch.Tensor, alpha: float) -> None:
+    """SPEC S9 in place on the device: t <- g / |g|, g = (1 - alpha) t + alpha f / |f| (fp32)."""
+    g = (1.0 - alpha) * t + alpha * (f / f.norm())
+    t.copy_(g / g.norm())
+
+
 def _dist_info(rank, world_size, group):
     if rank is not None and world_size is not None:
         return int(rank), int(world_size), group
@@ -177,14 +183,13 @@ class Tracker:
         return est
 
     def update_template(self, state, alpha: Optional[float] = None) -> None:
-        """Template update: t <- normalise((1 - alpha) t + alpha f / |f|) with f the CLS
-        feature of the crop at `state` = (x, y, scale) of the current frame. In place, so the captured graph
+        """Template update (SPEC S9): t <- normalise((1 - alpha) t + alpha f / |f|) with f the
+        CLS feature of the crop at `state` = (x, y, scale) of the current frame. In place, so the captured graph
         keeps reading the same buffer; every rank computes the same bits (same estimate, same kernels)."""
         a = self.template_alpha if alpha is None else float(alpha)
         st = torch.tensor([[state[0]], [state[1]], [state[2]]], dtype=torch.float32, device=self.device)
         f = self.engine.features(self._frame_dev, st, self.box_wh)[0]
-        t = (1.0 - a) * self.template + a * (f / f.norm())
-        self.template.copy_(t / t.norm())
+        _blend_template(self.template, f, a)
 
     # ------------------------------------------------------------------ checkpoint / resume (SURVEY.md §5)
     def config_fingerprint(self) -> dict:
@@ -271,11 +276,12 @@ class Tracker:
 
 
 class MultiTracker:
-    """Several targets in one frame loop: one ParticleFilter per target, and ONE batched
-    ViT forward over every target's particles per frame (crops with each target's own template box, one patch
+    """Several targets in one frame loop (SPEC S9): one ParticleFilter per target, and ONE
+    batched ViT forward over every target's particles per frame (crops with each target's own template box, one patch
     GEMM / encoder / final LN over all K*P crops, cosine weights against each target's own template), captured
     into one HIP graph. Target k's particle stream is seeded with particles.seed + k, so a MultiTracker with one
-    target reproduces Tracker bit for bit.
+    target reproduces Tracker bit for bit. With likelihood.template_update = alpha > 0 every target's template is
+    updated from its own estimate after each frame (one batched feature pass over the K estimate crops).
     Several ranks (as Tracker): every target's particles are sharded by index range over the ranks, each rank runs
     the ViT over its K x P/G crops, and each target's filter does its own chunk all-gather + global estimate /
     resample, so every rank returns the same K estimates, bit-identical to one rank."""
@@ -305,6 +311,7 @@ class MultiTracker:
                                 c["model"]["mean"], c["model"]["std"])
         self.lam = float(c["likelihood"]["lambda"])
         self.bits = int(c["likelihood"]["weight_bits"])
+        self.template_alpha = float(c["likelihood"]["template_update"])
         self.use_graph = bool(use_graph)
         self.pfs: List[ParticleFilter] = []
         self.templates: List[torch.Tensor] = []
@@ -362,6 +369,37 @@ class MultiTracker:
             self._forward()
         self._graph = g
 
+    def weigh(self) -> None:
+        """Crop + ViT + weights of every target's predicted particles on the uploaded frame (graph replay when
+        enabled); each filter's Q is set."""
+        if self.use_graph:
+            if self._graph is None:
+                self._capture()
+            self._graph.replay()
+        else:
+            self._forward()
+        for k, pf in enumerate(self.pfs):
+            pf.set_weights(self.engine.Q[k * self.n_local:(k + 1) * self.n_local])
+
+    def step(self) -> List[Tuple[float, float, float]]:
+        """Every target's estimate + resample (all enqueued, then one wait), then the template updates."""
+        for pf in self.pfs:
+            pf._settle()
+            pf._commit()
+        ests = [pf._read_estimate() for pf in self.pfs]
+        if self.template_alpha > 0.0:
+            self.update_templates(ests)
+        return ests
+
+    def update_templates(self, states, alpha: Optional[float] = None) -> None:
+        """SPEC S9 for every target: t_k <- normalise((1 - alpha) t_k + alpha f_k / |f_k|), f_k the feature of the crop
+        at states[k] with target k's box, all K crops in one batched pass. In place (the graph reads the buffers)."""
+        a = self.template_alpha if alpha is None else float(alpha)
+        sets = [torch.tensor([[st[0]], [st[1]], [st[2]]], dtype=torch.float32, device=self.device) for st in states]
+        f = self.engine.features_many(self._frame_dev, sets, self.boxes)
+        for k in range(self.K):
+            _blend_template(self.templates[k], f[k], a)
+
     def track(self, frame) -> List[Tuple[float, float, float]]:
         if not self.pfs:
             raise RuntimeError("call init(frame, bboxes) first")
@@ -370,14 +408,5 @@ class MultiTracker:
         for pf in self.pfs:
             pf.height, pf.width = int(fd.shape[0]), int(fd.shape[1])
             pf.predict(self.frame_index)
-        if self.use_graph:
-            if self._graph is None:
-                self._capture()
-            self._graph.replay()
-        else:
-            self._forward()
-        for k, pf in enumerate(self.pfs):       # every target's estimate + resample enqueued, then one wait
-            pf.set_weights(self.engine.Q[k * self.n_local:(k + 1) * self.n_local])
-            pf._settle()
-            pf._commit()
-        return [pf._read_estimate() for pf in self.pfs]
+        self.weigh()
+        return self.step()

@@ -203,9 +203,13 @@ class ViTEngine:
         self.h = torch.empty(n, N, D, device=dev, dtype=dt)
         self.x = torch.empty(n, N, D, device=dev, dtype=dt)
         self.qkv = torch.empty(n, N, 3 * D, device=dev, dtype=dt)
-        hid_elems = max(n * N * F, n * A.n_patches * A.patch_kp)
+        # hid: the bf16 MLP hidden of every token row; in fp8 mode FC1 writes MX8 (hid8) and the bf16 hidden holds only
+        # the last block's CLS rows, so it is sized for those (configs[4]: 7.4 GB less per 8192 particles). It also
+        # hosts the im2col patches (free until the first FC1).
+        hid_rows = n if self.fp8 else n * N
+        hid_elems = max(hid_rows * F, n * A.n_patches * A.patch_kp)
         self.hid_flat = torch.empty(hid_elems, device=dev, dtype=dt)
-        self.hid = self.hid_flat[: n * N * F].view(n * N, F)
+        self.hid = self.hid_flat[: hid_rows * F].view(hid_rows, F)
         self.patches = self.hid_flat[: n * A.n_patches * A.patch_kp].view(n * A.n_patches, A.patch_kp)
         self.stats = torch.empty(n * N, 2, device=dev, dtype=torch.float32)
         # bf16 fold mode: residual-stream statistics planes written by the GEMMs that produce h (patch embed,
@@ -452,6 +456,16 @@ class ViTEngine:
         n = particles.shape[1]
         assert n <= self.batch
         self.embed(frame, particles, box_wh)
+        self.encoder(n)
+        dummy_t = torch.zeros(self.arch.dim, device=self.device, dtype=torch.float32)
+        vpf.cls_weight(self.h[:n], self.ng, self.nb, self.arch.ln_eps, dummy_t, 0.0, 0, self.Q[:n], self.feat[:n],
+                       None)
+        return self.feat[:n]
+
+    def features_many(self, frame: torch.Tensor, particle_sets, boxes) -> torch.Tensor:
+        """LN'd CLS features [n][D] fp32 of several particle sets, set k cropped with its own box boxes[k] (the
+        multi-object template update); rows in set order. A crop's features do not depend on the batch."""
+        n = self.embed_many(frame, particle_sets, boxes)
         self.encoder(n)
         dummy_t = torch.zeros(self.arch.dim, device=self.device, dtype=torch.float32)
         vpf.cls_weight(self.h[:n], self.ng, self.nb, self.arch.ln_eps, dummy_t, 0.0, 0, self.Q[:n], self.feat[:n],
