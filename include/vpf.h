@@ -70,7 +70,7 @@ int vpf_cls_rows_f32(float* tokens, int64_t n_part, int N, int D, const float* c
  * g2 = patch_rows, M % g2 == 0); EPI_LN / EPI_LN_GELU (LayerNorm folded into the GEMM, A = the raw
  * residual stream): W = W * diag(gamma), colsum fp32[N] = sum_k W[n][k] (of the bf16 W), bias = b + W_orig beta,
  * and row_stats either (stats_parts == 0) fp32[M][2] = {mean, rstd} of A's rows (vpf_row_stats_*), or
- * (stats_parts = P in 1..16; 1..15 under vpf_gemm_tune kernel 2) fp32[P][M][2] planes of {sum, sumsq} over
+ * (stats_parts = P in 1..16) fp32[P][M][2] planes of {sum, sumsq} over
  * disjoint column blocks of A's rows (the stats_out of the GEMM that produced A), combined with eps = ln_eps:
  * rstd = 1/sqrt(sumsq/K - mean^2 + eps).
  * stats_out (EPI_BIAS_RESIDUAL / EPI_PATCH only, may be NULL): fp32[ceil(N/64)][R][2] planes, plane t =
@@ -96,18 +96,14 @@ int vpf_gemm_bf16_splitk(const uint16_t* A, int64_t lda, const uint16_t* W, cons
                          const uint16_t* residual, const float* row_stats, const float* colsum, uint16_t* C,
                          int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue, int splits, float* stats_out,
                          float* partial_ws, int64_t ws_elems, void* stream);
-/* Tuning knob for vpf_gemm_bf16 (process-wide; call it only between launches). kernel: 0 = the per-shape
- * defaults (the ping-pong kernel 5 for VPF_EPI_LN, the deep-ring kernel 1 otherwise; tile group 2 for N <= 1024,
- * 8 for VPF_EPI_LN_GELU, 4 otherwise; group ignored), 1 = the deep-ring kernel (3 A + 2 B K-tiles in LDS) for every shape, 2 = the 2-stage
- * ring (A/B timing; no fp8 output, <= 15 planes), 3-7 and 10-17 = A/B variants (gemm_bf16.hip; 17 = the mid-K-tile
- * barrier loop). group: A-panel group
- * size of the tile order for every shape, also used by vpf_gemm_mx8 (0 = row-major; < 0 = keep). Initial values: the
- * per-shape defaults, or VPF_GEMM_KERNEL / VPF_GEMM_GROUP when set. Every accepted kernel gives the same bits.
- * Kernels 8, 9, 24-26 and 28 (timing probes that do not write C: no stores / no epilogue / only the K loop's DMAs,
- * DMAs + fragment reads, DMAs + MFMAs / the 4-wave loop alone), 20-23 (cache-policy bits on the K-loop DMAs) and 27
- * (an L2 prefetch ahead of the DMAs; both same bits as kernel 1) exist only in a -DVPF_GEMM_LAB build (make lab ->
- * libvpf_lab.so); a product library returns VPF_ERR_ARG for them, as for an unknown kernel, and ignores them in
- * VPF_GEMM_KERNEL. */
+/* Kernel choice for vpf_gemm_bf16 (process-wide; call it only between launches; tests and A/B timing). The product
+ * library has two bf16 kernels and both give the same bits for every epilogue: kernel 1 = the deep-ring k_gemm_bf16
+ * (3 A + 2 B K-tiles in LDS), 5 = the ping-pong k_gemm_pp (<= 15 statistics planes; otherwise kernel 1's form).
+ * kernel 0 = the per-shape defaults (5 for VPF_EPI_LN, 1 otherwise; A-panel group 2 for N <= 1024, 8 for
+ * VPF_EPI_LN_GELU, 4 otherwise). kernel 1 / 5 apply to every shape, with group >= 0 as the A-panel group size of the
+ * tile order for every shape (also used by vpf_gemm_mx8; 0 = row-major) or -1 for the per-shape groups. Returns
+ * VPF_ERR_ARG for any other kernel (the A/B variants of earlier rounds are in the lab build, tools/gemm_lab) or a
+ * group outside [-1, 64]. Nothing in the library reads the environment. */
 int vpf_gemm_tune(int kernel, int group);
 
 /* MX8 operands (OCP MX-FP8: e4m3fn elements, one e8m0 scale per 32 consecutive K values):
@@ -155,6 +151,10 @@ int vpf_layernorm_f32(const float* x, int64_t rows, int D, int64_t x_stride, con
 /* H6: per (particle, head) softmax(q k^T * scale) v. qkv: [B][N][3][H][hd], out: [B][N][H][hd].
  * Only the first q_rows queries of every particle are computed (q_rows = N: all; 1: the CLS row, used by
  * the last encoder layer whose other rows feed nothing). hd == 64, N <= 640 (f32: N <= 4096, keys streamed through LDS in 128-key chunks). */
+/* Kernel choice for vpf_attention_bf16 at N <= 256 (process-wide, between launches; tests and A/B timing): 0 = the
+ * default persistent chunk-ring kernel, 1 = the one-workgroup-per-(particle, head) key-pipelined kernel, 2-3 = ring
+ * variants (chunks per barrier, ring slots) = (1, 8), (4, 8). All give the same bits. */
+int vpf_attention_tune(int variant);
 int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd,
                        float scale, int q_rows, void* stream);
 /* fp8 path: vpf_attention_bf16 (all N <= 256 query rows) writing its output as MX8 (out8 / s8: the A operand of

@@ -206,5 +206,8 @@ def test_product_library_has_no_knobs():
         for k in (1, 5):
             assert L.vpf_gemm_tune(k, -1) == 0
         assert L.vpf_gemm_tune(1, 999) == -1
+        assert L.vpf_attention_tune(4) == -1 and L.vpf_attention_tune(-1) == -1
+        assert L.vpf_attention_tune(1) == 0
     finally:
         assert L.vpf_gemm_tune(0, -1) == 0
+        assert L.vpf_attention_tune(0) == 0

@@ -1,8 +1,11 @@
 """Same-process A/B of the bf16 attention launch variants at the configs[1] shape (4096 particles x 12 heads, N = 197):
-rounds of (variant A, variant B, ...) launches, HIP-event time per launch, medians per variant. Variants are env
-settings the launcher reads per call (VPF_ATTN_TAIL16, VPF_ATTN_TAIL, VPF_ATTN_MODE).
+rounds of (variant A, variant B, ...) launches, HIP-event time per launch, medians per variant.
 
-    python tools/attn_ab.py [--particles 4096] [--rounds 15] [--n 197] ["VPF_ATTN_TAIL16=0" "VPF_ATTN_TAIL16=1" ...]
+Variants: "tune=<k>" = vpf_attention_tune(k) of the product library (0 = the persistent chunk ring, 1 = the one-unit
+key-pipelined kernel, 2 / 3 = other ring geometries); anything else is a set of environment settings for the lab library
+(VPF_LIB_PATH=.../libvpf_lab.so: VPF_ATTN_TAIL16, VPF_ATTN_TAIL, VPF_ATTN_MODE, VPF_ATTN_LAB).
+
+    python tools/attn_ab.py [--particles 4096] [--rounds 15] [--n 197] [tune=1 tune=0 ...]
 """
 from __future__ import annotations
 
@@ -21,11 +24,12 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--n", type=int, default=197)
     ap.add_argument("--heads", type=int, default=12)
-    ap.add_argument("variants", nargs="*", default=["VPF_ATTN_TAIL16=0", "VPF_ATTN_TAIL16=1"])
+    ap.add_argument("variants", nargs="*", default=["tune=1", "tune=0", "tune=2", "tune=3"])
     args = ap.parse_args()
     import torch
 
-    from vitparticlefiltertracker_amd import ops  # noqa: F401
+    from vitparticlefiltertracker_amd import _lib, ops  # noqa: F401
+    L = _lib.lib()
     P, N, H = args.particles, args.n, args.heads
     D = 64 * H
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -36,7 +40,10 @@ def main() -> int:
     def launch(v):
         for kv in v.split(","):
             k, val = kv.split("=")
-            os.environ[k] = val
+            if k == "tune":
+                assert L.vpf_attention_tune(int(val)) == 0
+            else:
+                os.environ[k] = val
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         torch.ops.vpf.attention(qkv, H, N, outs[v])

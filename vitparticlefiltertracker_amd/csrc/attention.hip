@@ -15,6 +15,7 @@
 //
 // fp32 parity path (vpf_attention_f32): one thread per query, K/V of the head in LDS as fp32, exact
 // expf softmax (N <= 256).
+#include <algorithm>
 #include <type_traits>
 
 #include "vpf_common.h"
@@ -59,6 +60,14 @@ __device__ __forceinline__ float xor32_max(float x) {
 __device__ __forceinline__ float xor32_sum(float x) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// the lane id through an opaque asm: address math derived from it stays where it is used (not hoisted into a loop's
+// live range)
+__device__ __forceinline__ int lane_id_opaque() {
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    return lane;
 }
 
 // One key step of T 32-key tiles (T = 1 or 2) for a 32-query strip: S^T = K Q^T on MFMA, online softmax
@@ -653,6 +662,187 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 
+// Persistent chunk-ring variant (round 4): the key-pipelined kernel's per-(particle, head) work, but a
+// workgroup is resident for many (particle, head) units and the K / V chunks stream through a ring of R 32-key slots
+// (8 KiB each: K rows | V rows, the same swizzled images as above at local row = key mod 32), so the DMA of the next
+// unit's first chunks runs under the current unit's last key steps instead of each workgroup loading its whole image
+// before it computes (the one-unit kernel's loads and compute overlapped only partly: 1.07 ms against 0.72 ms of loads
+// and 0.84 ms of compute alone, profiles/r3_lab/attn_load_compute_split.txt).
+//  * Grid: two 512-thread workgroups per CU (R x 8 KiB of LDS each); workgroup w takes units w, w + G, w + 2G, ...
+//  * Chunk stream: global chunk index g = j NT + c over this workgroup's units j and their chunks c; chunk g lives in
+//    slot g % R. Every wave issues exactly one DMA piece per chunk (waves 0-3: the chunk's four 8-row K pieces, 4-7: its
+//    V pieces), in g order; past the last chunk the pieces re-read the last chunk's rows into free slots (uniform
+//    counts, bytes never read).
+//  * Groups of CB chunks: at the top of group s a counted vmcnt (this wave's pieces of chunks s CB .. s CB + CB - 1
+//    landed; later pieces, the next unit's Q loads and the previous unit's stores may stay in flight) and one
+//    s_barrier (everyone's pieces landed, and everyone is done with group s - 1), then the refill of the group s - 1
+//    slots with chunks s CB + R - CB .. s CB + R - 1. The wait count is a closed form of (s, NT, R, CB, the wave's store
+//    count), checked against a simulation of the issue sequence (tools/sim/attn_ring_counts.py).
+//  * Unit boundary (before chunk j NT, j >= 1): the wave's Q fragments of unit j are loaded (asm, into the registers
+//    of unit j - 1, whose last QK^T has been consumed), then unit j - 1's output is stored, then a wave-local
+//    vmcnt(stores) pins Q (in-order retirement: the older ring pieces have landed by then as well).
+//  * Per query row the arithmetic is the one-unit kernel's (same step functions, same order): bit-identical output.
+// N <= 256 (one strip per wave), bf16 output.
+template <int CB, int R>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_ring(
+    const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, int BH, float scale_log2, int q_rows) {
+    static_assert(R >= 2 * CB, "the ring holds the group being computed and the group in flight");
+    __shared__ __attribute__((aligned(16))) char ring[R * 8192];
+    const int NP = (N + 31) & ~31;
+    const int NT = NP >> 5;
+    const int D = H * HD;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nstrips = (q_rows + 31) >> 5;
+    const int nlast = (N - 1) >> 5;
+    const bool w16 = wid == nlast && wid < nstrips && N - 32 * nlast <= 16;
+    const bool active = wid < nstrips;
+    const int S = active ? 4 : 0;          // output store instructions per unit of this wave
+    const int G = gridDim.x;
+    const int J = ((int)blockIdx.x < BH) ? (BH - 1 - (int)blockIdx.x) / G + 1 : 0;   // units of this workgroup
+    if (J == 0) return;                    // workgroup-uniform
+    const int Gtot = J * NT;
+    const int nfull = N >> 5;
+    auto unit_base = [&](int j) -> const bf16_t* {
+        const int bh = (int)blockIdx.x + j * G;
+        const int b = bh / H, h = bh - (bh / H) * H;
+        return qkv + (int64_t)b * N * 3 * D + h * HD;
+    };
+    // this wave's piece of chunk g (clamped to the last real chunk past the end) into slot g % R
+    const bool isv = wid >= 4;
+    // lane-derived addresses are recomputed where they are used (lane_id_opaque: not hoistable), so nothing of the
+    // DMA / Q / store address math stays live across the key steps (the one-unit kernel's 121 VGPRs are the budget)
+    auto issue = [&](int g) {
+        const int ln = lane_id_opaque();
+        const int sub = ln >> 3, pslot = ln & 7;
+        const int gc = min(g, Gtot - 1);
+        const int j = gc / NT, c = gc - (gc / NT) * NT;
+        const int rl = 8 * (wid & 3) + sub;            // local row in the chunk
+        const int ch = isv ? (pslot ^ (((rl >> 1) & 1) << 2)) : (pslot ^ ((rl >> 1) & 7));
+        const bf16_t* src = unit_base(j) + (isv ? 2 * D : D) + (int64_t)min(c * 32 + rl, N - 1) * 3 * D + ch * 8;
+        char* dst = ring + (g % R) * 8192 + (isv ? 4096 : 0) + (wid & 3) * 1024;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+    };
+    bf16x8 qf[4];
+    auto load_q = [&](int j) {   // one asm load per register, the strip kind in the address only (see the pipe kernel)
+        const int lane = lane_id_opaque();
+        const int l32 = lane & 31, hh = lane >> 5, q = wid * 32 + l32;
+        const bf16_t* qb = unit_base(j);
+        const bf16_t* qp = w16 ? qb + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
+                               : qb + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
+        const int step = w16 ? 32 : 16;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + (w16 ? (ks & 1) : ks) * step));
+    };
+    auto run = [&](auto k16) {
+        constexpr bool W16 = decltype(k16)::value;
+        // prologue inside each strip kind's path: Q of unit 0 (the oldest op), then the first R - CB pieces (qf is then
+        // not live across the strip-kind branch)
+        load_q(0);
+        for (int g = 0; g < R - CB; ++g) issue(g);
+        f32x16 o0 = {}, o1 = {};
+        f32x4 o16[4] = {};
+        float m = -INFINITY, l = 0.f;
+        auto finish_unit = [&](int j) {   // unit j's output rows (the pipe kernel's epilogues)
+            if (!active) return;
+            const int lane = lane_id_opaque();
+            const int l32 = lane & 31, hh = lane >> 5, q = wid * 32 + l32;
+            const int bh = (int)blockIdx.x + j * G;
+            const int b = bh / H, h = bh - (bh / H) * H;
+            const int64_t row0 = (int64_t)b * N;
+            if constexpr (W16) {
+                l = xor32_sum(xor16_sum(l));
+                const float inv = 1.0f / l;
+                const int qq = wid * 32 + (lane & 15);
+                bf16_t* orow = out + (row0 + min(qq, N - 1)) * D + h * HD + 4 * (lane >> 4);
+                if (qq < q_rows) {
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt)
+                        *reinterpret_cast<uint2*>(orow + 16 * dt) = make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
+                                                                              pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
+                }
+            } else {
+                l = xor32_sum(l);
+                const float inv = 1.0f / l;
+                uint32_t gx[8], gy[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const f32x16& o = k < 4 ? o0 : o1;
+                    const int b4 = 4 * (k & 3);
+                    gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
+                    gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
+                }
+                uint4 ov[4];
+#pragma unroll
+                for (int k = 0; k < 8; k += 2) {
+                    const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
+                    const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
+                    ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+                }
+                bf16_t* orow = out + (row0 + min(q, N - 1)) * D + h * HD + 8 * hh;
+                if (q < q_rows) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
+                }
+            }
+        };
+        // one loop over this workgroup's chunks; a group top every CB chunks (the barrier schedule depends on g only)
+        for (int g = 0; g < Gtot; ++g) {
+            const int j = g / NT, c = g - (g / NT) * NT;
+            if (g % CB == 0) {
+                // ops this wave issued after its piece of chunk s CB + CB - 1 (tools/sim/attn_ring_counts.py)
+                const int s = g / CB;
+                const int gl = s * CB + CB - 1;
+                const int s_issue = max(0, (gl - R + CB) / CB);
+                const int a = max(s_issue * CB, 1), b = s * CB;
+                const int bnd = b <= a ? 0 : (b - 1) / NT - (a - 1) / NT;
+                wait_vmcnt((R - 2 * CB) + (4 + S) * bnd);
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+#pragma unroll
+                for (int i = 0; i < CB; ++i) issue(s * CB + R - CB + i);   // into the slots of group s - 1
+            }
+            if (c == 0 && j > 0) {
+                // unit boundary: Q of unit j into the (dead) registers of unit j - 1, then unit j - 1's stores, then a
+                // wave-local wait for Q (the stores may stay in flight)
+                load_q(j);
+                finish_unit(j - 1);
+                if (S) asm volatile("s_waitcnt vmcnt(4)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
+                else asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
+                if constexpr (W16) {
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt) o16[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+                } else {
+                    o0 = f32x16{};
+                    o1 = f32x16{};
+                }
+                m = -INFINITY;
+                l = 0.f;
+            }
+            if (!active) continue;
+            // slot of chunk g, addressed with the global key base kb (the swizzles depend on key mod 32 only)
+            const int kb = c * 32;
+            const char* Ks = ring + (g % R) * 8192 - kb * ROWB;
+            const char* Vs = Ks + 4096;
+            if (c < nfull) {
+                if constexpr (W16) attn_step16<false>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o16);
+                else attn_step<1, false, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+            } else {
+                if constexpr (W16) attn_step16<true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o16);
+                else if (N - kb <= 8) attn_step_tail8(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+                else attn_step<1, true, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+            }
+        }
+        // the pieces past the last chunk: their group tops' refills were issued above; nothing waits for them but the
+        // final drain
+        finish_unit(J - 1);
+    };
+    if (w16) run(std::true_type{});
+    else run(std::false_type{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may outlive the workgroup
+}
+
 // CLS-only attention (q_rows == 1: the last encoder block, whose other query rows feed nothing): one wave
 // per (particle, head), 4 per workgroup, no LDS, so occupancy is set by VGPRs and many heads stream K / V
 // at once (the path is pure HBM streaming: 2 x N x 128 B per head for one query).
@@ -810,6 +1000,25 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ qkv,
 
 }  // namespace
 
+static int attn_cus() {   // compute units of the current device (the persistent kernel's grid)
+    static int cached = 0;
+    if (!cached) {
+        int dev = 0, n = 0;
+        cached = (hipGetDevice(&dev) == hipSuccess &&
+                  hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) ? n : 256;
+    }
+    return cached;
+}
+// Attention kernel choice for N <= 256: 0 = the default (k_attn_bf16_ring<2, 8>), 1 = the one-unit key-pipelined
+// kernel, 2-3 = ring variants (CB, R) = (1, 8), (4, 8). (Rings of 4 slots spill 3 VGPRs at the 128-VGPR limit.) Process state set by an explicit call (tests,
+// A/B), never read from the environment.
+static int g_attn_variant = 0;
+VPF_API int vpf_attention_tune(int variant) {
+    if (variant < 0 || variant > 3) return VPF_ERR_ARG;
+    g_attn_variant = variant;
+    return 0;
+}
+
 VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd, float scale,
                                int q_rows, void* stream) {
     if (B < 0 || N <= 0 || N > 640 || H <= 0 || hd != HD || B * H > INT32_MAX || q_rows < 1 || q_rows > N)
@@ -825,18 +1034,32 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
                            N, H, (int)BH, scale_log2);
         VPF_RETURN_LAUNCH();
     }
-    // N <= 256: the key-pipelined kernel (8 waves, one strip each); N > 256: the whole-image kernel (waves loop over
-    // strips)
+    // N <= 256: the persistent chunk-ring kernel (default) or the one-unit key-pipelined kernel (vpf_attention_tune 1);
+    // N > 256: the whole-image kernel (waves loop over strips). Both N <= 256 kernels give the same bits.
     if (N <= 256) {
-        static bool pipe_attr = false;   // benign race: idempotent attribute set
-        if (!pipe_attr) {
-            (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, false>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            pipe_attr = true;
+        if (g_attn_variant == 1) {
+            static bool pipe_attr = false;   // benign race: idempotent attribute set
+            if (!pipe_attr) {
+                (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, false>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                pipe_attr = true;
+            }
+            hipLaunchKernelGGL((k_attn_bf16_pipe<PIPE_CPB, false>), dim3((unsigned)(B * H)), dim3(512), lds,
+                               (hipStream_t)stream, qkv, reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows,
+                               (uint8_t*)nullptr, 0, (uint8_t*)nullptr, 0);
+            VPF_RETURN_LAUNCH();
         }
-        hipLaunchKernelGGL((k_attn_bf16_pipe<PIPE_CPB, false>), dim3((unsigned)(B * H)), dim3(512), lds,
-                           (hipStream_t)stream, qkv, reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows,
-                           (uint8_t*)nullptr, 0, (uint8_t*)nullptr, 0);
+        const int64_t BH = B * H;
+        const unsigned G = (unsigned)std::min<int64_t>(BH, 2 * (int64_t)attn_cus());
+        typedef void (*ring_fn)(const bf16_t*, bf16_t*, int, int, int, float, int);
+        ring_fn fn = k_attn_bf16_ring<2, 8>;
+        switch (g_attn_variant) {
+            case 2: fn = k_attn_bf16_ring<1, 8>; break;
+            case 3: fn = k_attn_bf16_ring<4, 8>; break;
+            default: break;
+        }
+        hipLaunchKernelGGL(fn, dim3(G), dim3(512), 0, (hipStream_t)stream, qkv, reinterpret_cast<bf16_t*>(out), N, H,
+                           (int)BH, scale_log2, q_rows);
         VPF_RETURN_LAUNCH();
     }
     const int threads = 64 * (strips < 8 ? strips : 8);
