@@ -334,7 +334,10 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            __builtin_amdgcn_s_barrier();
+            // LAB 13 (lab kernel 29, round 4): the K loop without its per-K-step barrier (each wave waits only for its own
+            // DMA pieces, then reads the tile whatever the other waves' pieces hold): a timing bound on what any
+            // wave-decoupled handshake could gain over the barrier; outputs are garbage
+            if constexpr (LAB != 13) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             if (!ILV && kt + 1 < nk) stage_b(kt + 1);
             if (!ILV && kt + 2 < nk) stage_a(kt + 2);
@@ -1266,6 +1269,10 @@ static int gemm_pf_dist() {   // kernel 27's prefetch distance in K-tiles (VPF_G
     else if (kern == 28 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                 \
         hipLaunchKernelGGL((k_gemm_w4<E, false, true, true>), grid, dim3(256), 0, s, VPF_GEMM_ARGS);           \
     }                                                                                                        \
+    else if (kern == 29 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                 \
+        hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 13>), grid, block, 0, s,      \
+                           VPF_GEMM_ARGS);                                                                   \
+    }                                                                                                        \
     else if (kern == 27 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                 \
         hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 12>), grid, block, 0, s,      \
                            A, (int)lda, W, bias, residual, pos, patch_rows,                                   \
@@ -1302,7 +1309,7 @@ constexpr bool kGemmLab = false;
 #define VPF_GEMM_LAB_LAUNCH(E)
 #endif
 static bool gemm_kernel_ok(int k) {
-    return (k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9))) || (kGemmLab && k >= 20 && k <= 28);
+    return (k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9))) || (kGemmLab && k >= 20 && k <= 29);
 }
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \

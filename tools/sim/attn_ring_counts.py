@@ -6,12 +6,12 @@ import itertools
 
 
 def ring_wait_count(s, NT, R, CB, S):
-    """The kernel's formula: ops issued after the piece of chunk s*CB + CB - 1, seen at group top s."""
+    """The kernel's formula: ops issued after the piece of chunk s*CB + CB - 1, seen at group top s. Unit boundaries
+    (the next unit's 4 Q loads + this unit's S stores) are issued after a unit's last chunk is computed, i.e. after
+    chunk m*NT - 1 for m = 1, 2, ...: those computed in groups s_issue .. s - 1 come after piece gl."""
     gl = s * CB + CB - 1
     s_issue = max(0, (gl - R + CB) // CB)          # group whose top issued piece gl (prologue -> 0)
-    a, b = s_issue * CB, s * CB
-    a = max(a, 1)
-    bound = 0 if b <= a else (b - 1) // NT - (a - 1) // NT
+    bound = (s * CB) // NT - (s_issue * CB) // NT
     return (R - 2 * CB) + (4 + S) * bound
 
 
@@ -29,9 +29,9 @@ def simulate(NT, R, CB, J, S):
         assert k == ring_wait_count(s, NT, R, CB, S), (NT, R, CB, J, S, s, k, ring_wait_count(s, NT, R, CB, S))
         for g in range(s * CB + R - CB, s * CB + R):      # refill after the barrier
             seq.append(("P", g))
-        for g in range(s * CB, min(s * CB + CB, G)):       # compute; unit boundary before chunk j*NT (j >= 1)
-            if g % NT == 0 and g > 0:
-                seq += [("Q", g // NT)] * 4 + [("S", g // NT - 1)] * S
+        for g in range(s * CB, min(s * CB + CB, G)):       # compute; unit boundary after the unit's last chunk
+            if g % NT == NT - 1:
+                seq += [("Q", g // NT + 1)] * 4 + [("S", g // NT)] * S
             # (the Q wait at the boundary is wave-local: vmcnt(S))
     return True
 

@@ -541,20 +541,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // The Q loads are older than this wave's NT DMA pieces: landed once at most NT are outstanding. Wait and pin the
     // registers HERE, before the strip-kind branch: the compiler copies asm-load destinations wherever register
     // allocation wants (the phi / live-range copies of the w16 branch below moved qf before any wait, reading stale
-    // registers: the round-2 NaN). The wait and the pin are ONE statement, so no copy of qf can be placed
-    // between them; the loads are the only earlier statements that write qf. The first chunk barrier waits for CPB
-    // chunks, so this costs nothing.
-    switch (NT) {   // NT = ceil(N / 32) <= 8 (N <= 256); the immediate must be a constant
-#define VPF_QWAIT(k)                                                                                             \
-    case k:                                                                                                      \
-        asm volatile("s_waitcnt vmcnt(" #k ")" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory"); \
-        break;
-        VPF_QWAIT(1) VPF_QWAIT(2) VPF_QWAIT(3) VPF_QWAIT(4) VPF_QWAIT(5) VPF_QWAIT(6) VPF_QWAIT(7) VPF_QWAIT(8)
-#undef VPF_QWAIT
-        default:
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
-            break;
-    }
+    // registers: the round-2 NaN). The first chunk barrier waits for CPB chunks, so this costs nothing.
+    // (Round 4: folding this wait and the pin into one asm statement per NT case, as ADVICE r3 suggested, made each qf a
+    // phi of several asm outputs again and brought the NaNs back: profiles/r4_pytest_gpu_a.log. The rule kept: no branch
+    // or merge between an asm load and the wait that retires it; the wait carries no register operands.)
+    wait_vmcnt(NT);
+    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
     const bool active = wid < nstrips;
     const int nfull = N >> 5;             // chunks without padded keys
     // The chunk loop, one template for both strip kinds: the barrier schedule (a counted wait + s_barrier before
@@ -678,9 +670,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 //    s_barrier (everyone's pieces landed, and everyone is done with group s - 1), then the refill of the group s - 1
 //    slots with chunks s CB + R - CB .. s CB + R - 1. The wait count is a closed form of (s, NT, R, CB, the wave's store
 //    count), checked against a simulation of the issue sequence (tools/sim/attn_ring_counts.py).
-//  * Unit boundary (before chunk j NT, j >= 1): the wave's Q fragments of unit j are loaded (asm, into the registers
-//    of unit j - 1, whose last QK^T has been consumed), then unit j - 1's output is stored, then a wave-local
-//    vmcnt(stores) pins Q (in-order retirement: the older ring pieces have landed by then as well).
+//  * Unit boundary (after the last chunk of every unit j): the wave's Q fragments of unit j + 1 are loaded (asm, into
+//    unit j's registers, whose last QK^T has been consumed), then unit j's output is stored, then a wave-local
+//    vmcnt(stores) retires Q (in-order retirement: the older ring pieces have landed by then as well).
 //  * Per query row the arithmetic is the one-unit kernel's (same step functions, same order): bit-identical output.
 // N <= 256 (one strip per wave), bf16 output.
 template <int CB, int R>
@@ -787,56 +779,56 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                 }
             }
         };
-        // one loop over this workgroup's chunks; a group top every CB chunks (the barrier schedule depends on g only)
-        for (int g = 0; g < Gtot; ++g) {
-            const int j = g / NT, c = g - (g / NT) * NT;
-            if (g % CB == 0) {
-                // ops this wave issued after its piece of chunk s CB + CB - 1 (tools/sim/attn_ring_counts.py)
-                const int s = g / CB;
-                const int gl = s * CB + CB - 1;
-                const int s_issue = max(0, (gl - R + CB) / CB);
-                const int a = max(s_issue * CB, 1), b = s * CB;
-                const int bnd = b <= a ? 0 : (b - 1) / NT - (a - 1) / NT;
-                wait_vmcnt((R - 2 * CB) + (4 + S) * bnd);
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        // unit loop / chunk loop; a group top every CB chunks of the global chunk index g = j NT + c (the barrier schedule
+        // depends on g only). The unit boundary code runs unconditionally at the end of every unit (no branch between
+        // the asm Q loads and the wait that retires them: a merge there made the round-2 / round-4 NaNs).
+        for (int j = 0; j < J; ++j) {
+            if constexpr (W16) {
 #pragma unroll
-                for (int i = 0; i < CB; ++i) issue(s * CB + R - CB + i);   // into the slots of group s - 1
-            }
-            if (c == 0 && j > 0) {
-                // unit boundary: Q of unit j into the (dead) registers of unit j - 1, then unit j - 1's stores, then a
-                // wave-local wait for Q (the stores may stay in flight)
-                load_q(j);
-                finish_unit(j - 1);
-                if (S) asm volatile("s_waitcnt vmcnt(4)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
-                else asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
-                if constexpr (W16) {
-#pragma unroll
-                    for (int dt = 0; dt < 4; ++dt) o16[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-                } else {
-                    o0 = f32x16{};
-                    o1 = f32x16{};
-                }
-                m = -INFINITY;
-                l = 0.f;
-            }
-            if (!active) continue;
-            // slot of chunk g, addressed with the global key base kb (the swizzles depend on key mod 32 only)
-            const int kb = c * 32;
-            const char* Ks = ring + (g % R) * 8192 - kb * ROWB;
-            const char* Vs = Ks + 4096;
-            if (c < nfull) {
-                if constexpr (W16) attn_step16<false>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o16);
-                else attn_step<1, false, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+                for (int dt = 0; dt < 4; ++dt) o16[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
             } else {
-                if constexpr (W16) attn_step16<true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o16);
-                else if (N - kb <= 8) attn_step_tail8(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
-                else attn_step<1, true, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+                o0 = f32x16{};
+                o1 = f32x16{};
             }
+            m = -INFINITY;
+            l = 0.f;
+            for (int c = 0; c < NT; ++c) {
+                const int g = j * NT + c;
+                if (g % CB == 0) {
+                    // ops this wave issued after its piece of chunk s CB + CB - 1 (tools/sim/attn_ring_counts.py)
+                    const int s = g / CB;
+                    const int gl = s * CB + CB - 1;
+                    const int s_issue = max(0, (gl - R + CB) / CB);
+                    // unit boundaries (4 Q loads + S stores, after a unit's last chunk) computed in groups s_issue .. s-1
+                    const int bnd = (s * CB) / NT - (s_issue * CB) / NT;
+                    wait_vmcnt((R - 2 * CB) + (4 + S) * bnd);
+                    __builtin_amdgcn_s_barrier();
+                    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+#pragma unroll
+                    for (int i = 0; i < CB; ++i) issue(s * CB + R - CB + i);   // into the slots of group s - 1
+                }
+                if (!active) continue;
+                // slot of chunk g, addressed with the global key base kb (the swizzles depend on key mod 32 only)
+                const int kb = c * 32;
+                const char* Ks = ring + (g % R) * 8192 - kb * ROWB;
+                const char* Vs = Ks + 4096;
+                if (c < nfull) {
+                    if constexpr (W16) attn_step16<false>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o16);
+                    else attn_step<1, false, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+                } else {
+                    if constexpr (W16) attn_step16<true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o16);
+                    else if (N - kb <= 8) attn_step_tail8(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+                    else attn_step<1, true, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+                }
+            }
+            // unit boundary: Q of the next unit (past the last unit: unit J - 1 again, never used) into the registers of
+            // this one (its last QK^T has been consumed), then this unit's stores, then a wave-local wait that retires Q
+            // (the S stores issued after it may stay in flight)
+            load_q(min(j + 1, J - 1));
+            finish_unit(j);
+            wait_vmcnt(S);
+            asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
         }
-        // the pieces past the last chunk: their group tops' refills were issued above; nothing waits for them but the
-        // final drain
-        finish_unit(J - 1);
     };
     if (w16) run(std::true_type{});
     else run(std::false_type{});
