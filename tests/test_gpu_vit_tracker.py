@@ -491,6 +491,10 @@ def test_checkpoint_resume_bit_exact(tmp_path, alpha):
             c2.setdefault(sect, {}).update(vals)
         with pytest.raises(ValueError, match=key):
             Tracker(load_config(c2), weights=w).load_checkpoint(path)
+    # explicit weights of another set (same seed in the config) are refused too
+    w2 = make_vit_weights(ARCHS["vit_tiny_patch16_224"], seed=4)
+    with pytest.raises(ValueError, match="weights_crc32"):
+        Tracker(cfg, weights=w2).load_checkpoint(path)
 
 
 def test_main_checkpoint_resume(tmp_path):

@@ -211,3 +211,17 @@ def test_product_library_has_no_knobs():
     finally:
         assert L.vpf_gemm_tune(0, -1) == 0
         assert L.vpf_attention_tune(0) == 0
+
+
+def test_weights_digest_tracks_the_weight_set():
+    """the checkpoint fingerprint's weights_crc32 depends on the tensors, not on the configured seed."""
+    from vitparticlefiltertracker_amd.config import ARCHS
+    from vitparticlefiltertracker_amd.tracker import weights_digest
+    from vitparticlefiltertracker_amd.weights import make_vit_weights
+    a = ARCHS["vit_tiny_patch16_224"]
+    d0, d0b, d1 = (weights_digest(make_vit_weights(a, seed=s)) for s in (0, 0, 1))
+    assert d0 == d0b and d0 != d1
+    w = make_vit_weights(a, seed=0)
+    w["blocks.3.mlp.fc1.bias"] = w["blocks.3.mlp.fc1.bias"].clone()
+    w["blocks.3.mlp.fc1.bias"][7] += 1e-3
+    assert weights_digest(w) != d0

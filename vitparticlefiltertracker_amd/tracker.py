@@ -26,6 +26,19 @@ from .vit import ViTEngine
 from .weights import make_vit_weights
 
 
+def weights_digest(weights) -> str:
+    """crc32 over every weight tensor's bytes (sorted names, fp32): the configuration fingerprint records it, so a
+    checkpoint taken with one weight set is refused by a tracker built with another, whether the weights came from
+    the seed or from the `weights=` argument."""
+    import zlib
+    crc = 0
+    for name in sorted(weights):
+        t = weights[name].detach().to("cpu", torch.float32).contiguous()
+        crc = zlib.crc32(name.encode(), crc)
+        crc = zlib.crc32(t.numpy().tobytes(), crc)
+    return f"{crc:08x}"
+
+
 def _blend_template(t: torch.Tensor, f: torch.Tensor, alpha: float) -> None:
     """SPEC S9 in place on the device: t <- g / |g|, g = (1 - alpha) t + alpha f / |f| (fp32)."""
     g = (1.0 - alpha) * t + alpha * (f / f.norm())
@@ -60,6 +73,7 @@ class Tracker:
             raise ValueError("particles.num must be divisible by the world size")
         self.n_local = P // self.world_size
         w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
+        self.weights_digest = weights_digest(w)
         self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, max(1, self.n_local),
                                 c["model"]["mean"], c["model"]["std"])
         self.lam = float(c["likelihood"]["lambda"])
@@ -198,6 +212,7 @@ class Tracker:
         c = self.cfg
         m, p, lk = c["model"], c["particles"], c["likelihood"]
         return {"arch": self.arch.name, "dtype": str(m["dtype"]), "weights_seed": int(m["weights"]["seed"]),
+                "weights_crc32": self.weights_digest,
                 "mean": [float(v) for v in m["mean"]], "std": [float(v) for v in m["std"]],
                 "P": int(p["num"]), "motion_std": [float(v) for v in p["motion_std"]],
                 "scale_range": [float(v) for v in p["scale_range"]], "seed": int(p["seed"]),
@@ -221,8 +236,13 @@ class Tracker:
 
     def load_state_dict(self, sd: dict) -> None:
         import json
-        if int(sd["format"]) != 2:
-            raise ValueError("unknown checkpoint format")
+        fmt = int(sd["format"])
+        if fmt == 1:
+            raise ValueError("checkpoint format 1 (rounds 1-2) records only P, rank, world size, seed and arch; format 2 "
+                             "also checks every value the tracking arithmetic depends on (dtype, lambda, motion, "
+                             "weights, ...): re-create the checkpoint with this version")
+        if fmt != 2:
+            raise ValueError(f"unknown checkpoint format {fmt}")
         c = self.cfg
         saved, mine = json.loads(str(sd["config"])), self.config_fingerprint()
         diff = sorted(k for k in set(saved) | set(mine) if saved.get(k) != mine.get(k))
