@@ -1,38 +1,53 @@
 """Design check for k_attn_bf16_ring's counted vmcnt waits (csrc/attention.hip): simulate one wave's vector-memory
-issue sequence (Q loads, one K/V DMA piece per chunk, output stores) and verify that the closed-form wait count the
-kernel uses at every group top equals the number of ops issued after the newest piece it needs (so the wait retires
-exactly that piece and everything older, with in-order retirement), for every (NT, R, CB, J, S) combination used."""
+issue sequence and verify that the closed-form wait counts the kernel uses equal the number of ops issued after the
+newest op each wait needs (so, with in-order retirement, the wait retires exactly that op and everything older), for
+every (NT, R, CB, J, S) combination.
+
+Per wave, in issue order:
+  prologue: Q(0) pieces x4 (the wave's query strip of unit 0 -> its LDS Q area), chunk pieces 0 .. R-CB-1;
+  for every unit j, for every chunk c (g = j NT + c):
+    group top (g % CB == 0): wait for the piece of chunk g + CB - 1 [k_gt], barrier, pieces g+R-CB .. g+R-1;
+    unit start (c == 0): wait for the Q(j) pieces [k_qw], read Q(j) from LDS, then Q(j+1) pieces x4;
+    compute chunk g;
+  unit end: S output stores."""
 import itertools
 
 
-def ring_wait_count(s, NT, R, CB, S):
-    """The kernel's formula: ops issued after the piece of chunk s*CB + CB - 1, seen at group top s. Unit boundaries
-    (the next unit's 4 Q loads + this unit's S stores) are issued after a unit's last chunk is computed, i.e. after
-    chunk m*NT - 1 for m = 1, 2, ...: those computed in groups s_issue .. s - 1 come after piece gl."""
+def k_gt(s, NT, R, CB, S):
+    """Ops issued after the piece of chunk gl = s CB + CB - 1, seen at group top s."""
     gl = s * CB + CB - 1
-    s_issue = max(0, (gl - R + CB) // CB)          # group whose top issued piece gl (prologue -> 0)
-    bound = (s * CB) // NT - (s_issue * CB) // NT
-    return (R - 2 * CB) + (4 + S) * bound
+    si = max(0, (gl - R + CB) // CB)      # group whose top issued piece gl (prologue -> 0)
+    a, b = si * CB, s * CB
+    nq = (b - 1) // NT - (a - 1) // NT if b > a else 0          # unit starts j NT in [a, b)  (j >= 0)
+    ns = b // NT - a // NT                                       # unit ends m NT in (a, b]  (m >= 1)
+    return (R - 2 * CB) + 4 * nq + S * ns
+
+
+def k_qw(j, NT, R, CB, S):
+    """Ops issued after the last Q(j) piece, seen at unit j's start (after the group top of chunk j NT, if any)."""
+    if j == 0:
+        return R   # Q(0) is the oldest op: the R - CB prologue pieces and group top 0's CB pieces follow it
+    gts = (j * NT) // CB - ((j - 1) * NT) // CB                  # group tops in ((j-1) NT, j NT]
+    return CB * gts + S
 
 
 def simulate(NT, R, CB, J, S):
     G = J * NT
-    seq = []              # op tags in issue order
-    seq += [("Q", 0)] * 4
-    for g in range(R - CB):
-        seq.append(("P", g))
-    ngroups = (G + CB - 1) // CB
-    for s in range(ngroups):
-        gl = s * CB + CB - 1
-        need = max(i for i, t in enumerate(seq) if t == ("P", gl))
-        k = len(seq) - 1 - need
-        assert k == ring_wait_count(s, NT, R, CB, S), (NT, R, CB, J, S, s, k, ring_wait_count(s, NT, R, CB, S))
-        for g in range(s * CB + R - CB, s * CB + R):      # refill after the barrier
-            seq.append(("P", g))
-        for g in range(s * CB, min(s * CB + CB, G)):       # compute; unit boundary after the unit's last chunk
-            if g % NT == NT - 1:
-                seq += [("Q", g // NT + 1)] * 4 + [("S", g // NT)] * S
-            # (the Q wait at the boundary is wave-local: vmcnt(S))
+    seq = [("Q", 0)] * 4 + [("P", g) for g in range(R - CB)]
+
+    def after(tag):
+        return len(seq) - 1 - max(i for i, t in enumerate(seq) if t == tag)
+    for j in range(J):
+        for c in range(NT):
+            g = j * NT + c
+            if g % CB == 0:
+                s = g // CB
+                assert after(("P", s * CB + CB - 1)) == k_gt(s, NT, R, CB, S), ("gt", NT, R, CB, J, S, s)
+                seq += [("P", x) for x in range(s * CB + R - CB, s * CB + R)]
+            if c == 0:
+                assert after(("Q", j)) == k_qw(j, NT, R, CB, S), ("qw", NT, R, CB, J, S, j)
+                seq += [("Q", j + 1)] * 4
+        seq += [("S", j)] * S
     return True
 
 

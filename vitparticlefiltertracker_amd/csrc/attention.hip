@@ -660,30 +660,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 // unit's first chunks runs under the current unit's last key steps instead of each workgroup loading its whole image
 // before it computes (the one-unit kernel's loads and compute overlapped only partly: 1.07 ms against 0.72 ms of loads
 // and 0.84 ms of compute alone, profiles/r3_lab/attn_load_compute_split.txt).
-//  * Grid: two 512-thread workgroups per CU (R x 8 KiB of LDS each); workgroup w takes units w, w + G, w + 2G, ...
+//  * Grid: two 512-thread workgroups per CU (R x 8 KiB + 32 KiB of LDS each); workgroup w takes units w, w + G, ...
 //  * Chunk stream: global chunk index g = j NT + c over this workgroup's units j and their chunks c; chunk g lives in
 //    slot g % R. Every wave issues exactly one DMA piece per chunk (waves 0-3: the chunk's four 8-row K pieces, 4-7: its
 //    V pieces), in g order; past the last chunk the pieces re-read the last chunk's rows into free slots (uniform
 //    counts, bytes never read).
-//  * Groups of CB chunks: at the top of group s a counted vmcnt (this wave's pieces of chunks s CB .. s CB + CB - 1
-//    landed; later pieces, the next unit's Q loads and the previous unit's stores may stay in flight) and one
-//    s_barrier (everyone's pieces landed, and everyone is done with group s - 1), then the refill of the group s - 1
-//    slots with chunks s CB + R - CB .. s CB + R - 1. The wait count is a closed form of (s, NT, R, CB, the wave's store
-//    count), checked against a simulation of the issue sequence (tools/sim/attn_ring_counts.py).
-//  * Unit boundary (after the last chunk of every unit j): the wave's Q fragments of unit j + 1 are loaded (asm, into
-//    unit j's registers, whose last QK^T has been consumed), then unit j's output is stored, then a wave-local
-//    vmcnt(stores) retires Q (in-order retirement: the older ring pieces have landed by then as well).
+//  * Queries: each wave's 32-row query strip also arrives by LDS-DMA, into a 4 KiB area of its own (K-image layout),
+//    one unit ahead: at unit j's start the wave reads Q(j) into registers and issues Q(j + 1)'s four pieces. (v1 loaded
+//    Q into registers at each unit boundary; waiting for those loads retired every older ring piece too - in-order
+//    vmcnt - so the ring drained at every unit: 1.54 ms against 1.06, profiles/r4_attn_ring_ab_v1.txt.)
+//  * Groups of CB chunks: at the top of group s a counted vmcnt (this wave's pieces of chunks up to s CB + CB - 1
+//    landed) and one s_barrier (everyone's pieces landed, and everyone is done with group s - 1), then the refill of the
+//    group s - 1 slots with chunks s CB + R - CB .. s CB + R - 1. Every wait count is a closed form of (s or j, NT, R,
+//    CB, the wave's store count) checked against a simulation of the issue sequence (tools/sim/attn_ring_counts.py).
 //  * Per query row the arithmetic is the one-unit kernel's (same step functions, same order): bit-identical output.
 // N <= 256 (one strip per wave), bf16 output.
 template <int CB, int R>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_ring(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, int BH, float scale_log2, int q_rows) {
     static_assert(R >= 2 * CB, "the ring holds the group being computed and the group in flight");
-    __shared__ __attribute__((aligned(16))) char ring[R * 8192];
+    __shared__ __attribute__((aligned(16))) char ring[R * 8192 + 8 * 4096];
     const int NP = (N + 31) & ~31;
     const int NT = NP >> 5;
     const int D = H * HD;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nstrips = (q_rows + 31) >> 5;
     const int nlast = (N - 1) >> 5;
@@ -695,16 +695,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     if (J == 0) return;                    // workgroup-uniform
     const int Gtot = J * NT;
     const int nfull = N >> 5;
+    char* qarea = ring + R * 8192 + wid * 4096;   // this wave's query strip (K-image layout, rows = strip rows)
     auto unit_base = [&](int j) -> const bf16_t* {
         const int bh = (int)blockIdx.x + j * G;
         const int b = bh / H, h = bh - (bh / H) * H;
         return qkv + (int64_t)b * N * 3 * D + h * HD;
     };
-    // this wave's piece of chunk g (clamped to the last real chunk past the end) into slot g % R
-    const bool isv = wid >= 4;
     // lane-derived addresses are recomputed where they are used (lane_id_opaque: not hoistable), so nothing of the
-    // DMA / Q / store address math stays live across the key steps (the one-unit kernel's 121 VGPRs are the budget)
-    auto issue = [&](int g) {
+    // DMA / Q / store address math stays live across the key steps
+    const bool isv = wid >= 4;
+    auto issue = [&](int g) {   // this wave's piece of chunk g (clamped past the end) into slot g % R
         const int ln = lane_id_opaque();
         const int sub = ln >> 3, pslot = ln & 7;
         const int gc = min(g, Gtot - 1);
@@ -715,73 +715,37 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         char* dst = ring + (g % R) * 8192 + (isv ? 4096 : 0) + (wid & 3) * 1024;
         __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
     };
-    bf16x8 qf[4];
-    auto load_q = [&](int j) {   // one asm load per register, the strip kind in the address only (see the pipe kernel)
-        const int lane = lane_id_opaque();
-        const int l32 = lane & 31, hh = lane >> 5, q = wid * 32 + l32;
-        const bf16_t* qb = unit_base(j);
-        const bf16_t* qp = w16 ? qb + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
-                               : qb + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
-        const int step = w16 ? 32 : 16;
+    auto issue_q = [&](int j) {   // the four 8-row pieces of this wave's query strip of unit min(j, J - 1)
+        const int ln = lane_id_opaque();
+        const int sub = ln >> 3, pslot = ln & 7;
+        const bf16_t* qb = unit_base(min(j, J - 1));
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + (w16 ? (ks & 1) : ks) * step));
+        for (int i = 0; i < 4; ++i) {
+            const int rl = 8 * i + sub;
+            const int ch = pslot ^ ((rl >> 1) & 7);
+            __builtin_amdgcn_global_load_lds((gptr_t)(qb + (int64_t)min(wid * 32 + rl, N - 1) * 3 * D + ch * 8),
+                                             (lptr_t)(qarea + i * 1024), 16, 0, 0);
+        }
     };
+    // ops issued after the piece of chunk s CB + CB - 1, at group top s (tools/sim/attn_ring_counts.py k_gt)
+    auto k_gt = [&](int s) {
+        const int gl = s * CB + CB - 1;
+        const int si = max(0, (gl - R + CB) / CB);
+        const int a = si * CB, b = s * CB;
+        const int nq = b > a ? (b - 1) / NT - (a == 0 ? -1 : (a - 1) / NT) : 0;   // unit starts in [a, b)
+        const int ns = b / NT - a / NT;                                             // unit ends in (a, b]
+        return (R - 2 * CB) + 4 * nq + S * ns;
+    };
+    // ops issued after the last Q(j) piece, at unit j's start (k_qw)
+    auto k_qw = [&](int j) { return j == 0 ? R : CB * ((j * NT) / CB - ((j - 1) * NT) / CB) + S; };
+    bf16x8 qf[4];
     auto run = [&](auto k16) {
         constexpr bool W16 = decltype(k16)::value;
-        // prologue inside each strip kind's path: Q of unit 0 (the oldest op), then the first R - CB pieces (qf is then
-        // not live across the strip-kind branch)
-        load_q(0);
+        issue_q(0);
         for (int g = 0; g < R - CB; ++g) issue(g);
         f32x16 o0 = {}, o1 = {};
         f32x4 o16[4] = {};
         float m = -INFINITY, l = 0.f;
-        auto finish_unit = [&](int j) {   // unit j's output rows (the pipe kernel's epilogues)
-            if (!active) return;
-            const int lane = lane_id_opaque();
-            const int l32 = lane & 31, hh = lane >> 5, q = wid * 32 + l32;
-            const int bh = (int)blockIdx.x + j * G;
-            const int b = bh / H, h = bh - (bh / H) * H;
-            const int64_t row0 = (int64_t)b * N;
-            if constexpr (W16) {
-                l = xor32_sum(xor16_sum(l));
-                const float inv = 1.0f / l;
-                const int qq = wid * 32 + (lane & 15);
-                bf16_t* orow = out + (row0 + min(qq, N - 1)) * D + h * HD + 4 * (lane >> 4);
-                if (qq < q_rows) {
-#pragma unroll
-                    for (int dt = 0; dt < 4; ++dt)
-                        *reinterpret_cast<uint2*>(orow + 16 * dt) = make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
-                                                                              pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
-                }
-            } else {
-                l = xor32_sum(l);
-                const float inv = 1.0f / l;
-                uint32_t gx[8], gy[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const f32x16& o = k < 4 ? o0 : o1;
-                    const int b4 = 4 * (k & 3);
-                    gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
-                    gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
-                }
-                uint4 ov[4];
-#pragma unroll
-                for (int k = 0; k < 8; k += 2) {
-                    const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
-                    const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
-                    ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
-                }
-                bf16_t* orow = out + (row0 + min(q, N - 1)) * D + h * HD + 8 * hh;
-                if (q < q_rows) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
-                }
-            }
-        };
-        // unit loop / chunk loop; a group top every CB chunks of the global chunk index g = j NT + c (the barrier schedule
-        // depends on g only). The unit boundary code runs unconditionally at the end of every unit (no branch between
-        // the asm Q loads and the wait that retires them: a merge there made the round-2 / round-4 NaNs).
         for (int j = 0; j < J; ++j) {
             if constexpr (W16) {
 #pragma unroll
@@ -795,23 +759,42 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             for (int c = 0; c < NT; ++c) {
                 const int g = j * NT + c;
                 if (g % CB == 0) {
-                    // ops this wave issued after its piece of chunk s CB + CB - 1 (tools/sim/attn_ring_counts.py)
-                    const int s = g / CB;
-                    const int gl = s * CB + CB - 1;
-                    const int s_issue = max(0, (gl - R + CB) / CB);
-                    // unit boundaries (4 Q loads + S stores, after a unit's last chunk) computed in groups s_issue .. s-1
-                    const int bnd = (s * CB) / NT - (s_issue * CB) / NT;
-                    wait_vmcnt((R - 2 * CB) + (4 + S) * bnd);
+                    wait_vmcnt(k_gt(g / CB));
                     __builtin_amdgcn_s_barrier();
-                    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+                    asm volatile("" ::: "memory");
 #pragma unroll
-                    for (int i = 0; i < CB; ++i) issue(s * CB + R - CB + i);   // into the slots of group s - 1
+                    for (int i = 0; i < CB; ++i) issue(g + R - CB + i);   // into the slots of group s - 1
+                }
+                if (c == 0) {
+                    // Q(j) from this wave's LDS area into registers, then Q(j + 1)'s DMA into the area (after the reads
+                    // have completed: lgkmcnt(0))
+                    wait_vmcnt(k_qw(j));
+                    asm volatile("" ::: "memory");
+                    {
+                        const int ln = lane_id_opaque();
+                        if constexpr (W16) {
+                            const int r16 = ln & 15, g4 = ln >> 4;
+#pragma unroll
+                            for (int kk = 0; kk < 4; ++kk)
+                                qf[kk] = *reinterpret_cast<const bf16x8*>(qarea + k_off(r16, 4 * (kk & 1) + g4));
+                        } else {
+                            const int l32 = ln & 31, hh = ln >> 5;
+#pragma unroll
+                            for (int ks = 0; ks < 4; ++ks)
+                                qf[ks] = *reinterpret_cast<const bf16x8*>(qarea + k_off(l32, ks * 2 + hh));
+                        }
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
+                    issue_q(j + 1);
                 }
                 if (!active) continue;
                 // slot of chunk g, addressed with the global key base kb (the swizzles depend on key mod 32 only)
                 const int kb = c * 32;
                 const char* Ks = ring + (g % R) * 8192 - kb * ROWB;
                 const char* Vs = Ks + 4096;
+                // the lane id re-read per step: the steps' lane-derived LDS addresses are then computed in the step,
+                // not hoisted out of both loops (which held ~10 VGPRs across them and spilled at the 128 limit)
+                const int lane = lane_id_opaque();
                 if (c < nfull) {
                     if constexpr (W16) attn_step16<false>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o16);
                     else attn_step<1, false, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
@@ -821,13 +804,50 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                     else attn_step<1, true, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
                 }
             }
-            // unit boundary: Q of the next unit (past the last unit: unit J - 1 again, never used) into the registers of
-            // this one (its last QK^T has been consumed), then this unit's stores, then a wave-local wait that retires Q
-            // (the S stores issued after it may stay in flight)
-            load_q(min(j + 1, J - 1));
-            finish_unit(j);
-            wait_vmcnt(S);
-            asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+            // unit j's output rows (the pipe kernel's epilogues): S store instructions
+            if (active) {
+                const int ln = lane_id_opaque();
+                const int bh = (int)blockIdx.x + j * G;
+                const int b = bh / H, h = bh - (bh / H) * H;
+                const int64_t row0 = (int64_t)b * N;
+                if constexpr (W16) {
+                    l = xor32_sum(xor16_sum(l));
+                    const float inv = 1.0f / l;
+                    const int qq = wid * 32 + (ln & 15);
+                    bf16_t* orow = out + (row0 + min(qq, N - 1)) * D + h * HD + 4 * (ln >> 4);
+                    if (qq < q_rows) {
+#pragma unroll
+                        for (int dt = 0; dt < 4; ++dt)
+                            *reinterpret_cast<uint2*>(orow + 16 * dt) =
+                                make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
+                                           pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
+                    }
+                } else {
+                    const int q = wid * 32 + (ln & 31), hh = ln >> 5;
+                    l = xor32_sum(l);
+                    const float inv = 1.0f / l;
+                    uint32_t gx[8], gy[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const f32x16& o = k < 4 ? o0 : o1;
+                        const int b4 = 4 * (k & 3);
+                        gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
+                        gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
+                    }
+                    uint4 ov[4];
+#pragma unroll
+                    for (int k = 0; k < 8; k += 2) {
+                        const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
+                        const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
+                        ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+                    }
+                    bf16_t* orow = out + (row0 + min(q, N - 1)) * D + h * HD + 8 * hh;
+                    if (q < q_rows) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
+                    }
+                }
+            }
         }
     };
     if (w16) run(std::true_type{});
@@ -1001,8 +1021,8 @@ static int attn_cus() {   // compute units of the current device (the persistent
     }
     return cached;
 }
-// Attention kernel choice for N <= 256: 0 = the default (k_attn_bf16_ring<2, 8>), 1 = the one-unit key-pipelined
-// kernel, 2-3 = ring variants (CB, R) = (1, 8), (4, 8). (Rings of 4 slots spill 3 VGPRs at the 128-VGPR limit.) Process state set by an explicit call (tests,
+// Attention kernel choice for N <= 256: 0 = k_attn_bf16_ring<2, 6>, 1 = the one-unit key-pipelined kernel, 2-3 = ring
+// variants (CB, R) = (3, 6), (1, 6). Process state set by an explicit call (tests,
 // A/B), never read from the environment.
 static int g_attn_variant = 0;
 VPF_API int vpf_attention_tune(int variant) {
@@ -1044,10 +1064,10 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
         const int64_t BH = B * H;
         const unsigned G = (unsigned)std::min<int64_t>(BH, 2 * (int64_t)attn_cus());
         typedef void (*ring_fn)(const bf16_t*, bf16_t*, int, int, int, float, int);
-        ring_fn fn = k_attn_bf16_ring<2, 8>;
+        ring_fn fn = k_attn_bf16_ring<2, 6>;
         switch (g_attn_variant) {
-            case 2: fn = k_attn_bf16_ring<1, 8>; break;
-            case 3: fn = k_attn_bf16_ring<4, 8>; break;
+            case 2: fn = k_attn_bf16_ring<3, 6>; break;
+            case 3: fn = k_attn_bf16_ring<1, 6>; break;
             default: break;
         }
         hipLaunchKernelGGL(fn, dim3(G), dim3(512), 0, (hipStream_t)stream, qkv, reinterpret_cast<bf16_t*>(out), N, H,
