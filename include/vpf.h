@@ -151,10 +151,6 @@ int vpf_layernorm_f32(const float* x, int64_t rows, int D, int64_t x_stride, con
 /* H6: per (particle, head) softmax(q k^T * scale) v. qkv: [B][N][3][H][hd], out: [B][N][H][hd].
  * Only the first q_rows queries of every particle are computed (q_rows = N: all; 1: the CLS row, used by
  * the last encoder layer whose other rows feed nothing). hd == 64, N <= 640 (f32: N <= 4096, keys streamed through LDS in 128-key chunks). */
-/* Kernel choice for vpf_attention_bf16 at N <= 256 (process-wide, between launches; tests and A/B timing): 0 = the
- * default persistent chunk-ring kernel, 1 = the one-workgroup-per-(particle, head) key-pipelined kernel, 2-3 = ring
- * variants (chunks per barrier, ring slots) = (3, 6), (1, 6). All give the same bits. */
-int vpf_attention_tune(int variant);
 int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd,
                        float scale, int q_rows, void* stream);
 /* fp8 path: vpf_attention_bf16 (all N <= 256 query rows) writing its output as MX8 (out8 / s8: the A operand of

@@ -549,38 +549,6 @@ def test_attention_bf16_large(B, N, H):
     assert torch.all(part[:, 1:] == 5.0)
 
 
-@pytest.mark.parametrize("B,N,H", [(4096, 197, 12), (300, 197, 12), (90, 256, 12), (80, 111, 12), (70, 33, 6),
-                                   (5, 1, 3), (2, 100, 1), (1, 197, 12), (600, 64, 2)])
-def test_attention_ring_equals_pipe(B, N, H):
-    """The persistent chunk-ring kernel (the default for N <= 256: workgroups resident for many (particle, head) units,
-    K / V chunks streaming through an LDS ring, counted waits from a closed form checked by tools/sim/attn_ring_counts.py)
-    against the one-unit key-pipelined kernel (vpf_attention_tune 1) and the other ring geometries (2, 3): bit-identical
-    for every row, including units per workgroup from 1 (B*H < 512) to 96 (configs[1]), odd tails (N = 33, 111, 197),
-    the 16-query tail strip and q_rows < N."""
-    from vitparticlefiltertracker_amd import _lib
-    L = _lib.lib()
-    torch.manual_seed(B + N + H)
-    D = 64 * H
-    qkv = (torch.randn(B, N, 3 * D, device=DEV) * 1.5).to(torch.bfloat16)
-    try:
-        outs = {}
-        for v in (1, 0, 2, 3):
-            assert L.vpf_attention_tune(v) == 0
-            for qr in sorted({N, max(1, N - 7), 2} if N > 2 else {N}):
-                o = torch.full((B, N, D), 3.0, device=DEV, dtype=torch.bfloat16)
-                vpf().attention(qkv, H, qr, o)
-                outs[(v, qr)] = o
-        torch.cuda.synchronize()
-        for (v, qr), o in outs.items():
-            ref = outs[(1, qr)]
-            bad = (o.view(torch.int16) != ref.view(torch.int16)).sum().item()
-            assert bad == 0, (v, qr, bad)
-            if qr > 1:
-                assert torch.all(o[:, qr:] == 3.0)
-    finally:
-        L.vpf_attention_tune(0)
-
-
 def test_attention_bf16_rescale_branch():
     """The lazy online-softmax rescale only runs when a query's max grows by > 2^8 (exp2 domain) within a
     key tile: force it (a key row aligned with a query, late in the sequence) and also plant spikes below the

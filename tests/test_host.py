@@ -195,7 +195,8 @@ def test_product_library_has_no_knobs():
                          check=True).stdout
     assert "getenv" not in dyn and "secure_getenv" not in dyn, dyn
     blob = open(_lib.LIB_PATH, "rb").read()
-    for lab_kernel in (b"k_gemm_pt", b"k_gemm_w4", b"attn_qk32", b"attn_sm_pv32", b"k_crop_patches_fast"):
+    for lab_kernel in (b"k_gemm_pt", b"k_gemm_w4", b"attn_qk32", b"attn_sm_pv32", b"k_crop_patches_fast",
+                       b"k_attn_bf16_ring"):
         assert lab_kernel not in blob, lab_kernel
     for product_kernel in (b"k_gemm_bf16", b"k_gemm_pp", b"k_gemm_mx8", b"k_attn_bf16_pipe", b"k_crop_patches_lds"):
         assert product_kernel in blob, product_kernel
@@ -206,11 +207,8 @@ def test_product_library_has_no_knobs():
         for k in (1, 5):
             assert L.vpf_gemm_tune(k, -1) == 0
         assert L.vpf_gemm_tune(1, 999) == -1
-        assert L.vpf_attention_tune(4) == -1 and L.vpf_attention_tune(-1) == -1
-        assert L.vpf_attention_tune(1) == 0
     finally:
         assert L.vpf_gemm_tune(0, -1) == 0
-        assert L.vpf_attention_tune(0) == 0
 
 
 def test_weights_digest_tracks_the_weight_set():

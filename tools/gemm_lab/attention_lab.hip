@@ -15,6 +15,7 @@
 //
 // fp32 parity path (vpf_attention_f32): one thread per query, K/V of the head in LDS as fp32, exact
 // expf softmax (N <= 256).
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -808,6 +809,207 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 
+// Persistent chunk-ring variant (round 4): the key-pipelined kernel's per-(particle, head) work, but a
+// workgroup is resident for many (particle, head) units and the K / V chunks stream through a ring of R 32-key slots
+// (8 KiB each: K rows | V rows, the same swizzled images as above at local row = key mod 32), so the DMA of the next
+// unit's first chunks runs under the current unit's last key steps instead of each workgroup loading its whole image
+// before it computes (the one-unit kernel's loads and compute overlapped only partly: 1.07 ms against 0.72 ms of loads
+// and 0.84 ms of compute alone, profiles/r3_lab/attn_load_compute_split.txt).
+//  * Grid: two 512-thread workgroups per CU (R x 8 KiB + 32 KiB of LDS each); workgroup w takes units w, w + G, ...
+//  * Chunk stream: global chunk index g = j NT + c over this workgroup's units j and their chunks c; chunk g lives in
+//    slot g % R. Every wave issues exactly one DMA piece per chunk (waves 0-3: the chunk's four 8-row K pieces, 4-7: its
+//    V pieces), in g order; past the last chunk the pieces re-read the last chunk's rows into free slots (uniform
+//    counts, bytes never read).
+//  * Queries: each wave's 32-row query strip also arrives by LDS-DMA, into a 4 KiB area of its own (K-image layout),
+//    one unit ahead: at unit j's start the wave reads Q(j) into registers and issues Q(j + 1)'s four pieces. (v1 loaded
+//    Q into registers at each unit boundary; waiting for those loads retired every older ring piece too - in-order
+//    vmcnt - so the ring drained at every unit: 1.54 ms against 1.06, profiles/r4_attn_ring_ab_v1.txt.)
+//  * Groups of CB chunks: at the top of group s a counted vmcnt (this wave's pieces of chunks up to s CB + CB - 1
+//    landed) and one s_barrier (everyone's pieces landed, and everyone is done with group s - 1), then the refill of the
+//    group s - 1 slots with chunks s CB + R - CB .. s CB + R - 1. Every wait count is a closed form of (s or j, NT, R,
+//    CB, the wave's store count) checked against a simulation of the issue sequence (tools/sim/attn_ring_counts.py).
+//  * Per query row the arithmetic is the one-unit kernel's (same step functions, same order): bit-identical output.
+// N <= 256 (one strip per wave), bf16 output.
+template <int CB, int R>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_ring(
+    const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, int BH, float scale_log2, int q_rows) {
+    static_assert(R >= 2 * CB, "the ring holds the group being computed and the group in flight");
+    __shared__ __attribute__((aligned(16))) char ring[R * 8192 + 8 * 4096];
+    const int NP = (N + 31) & ~31;
+    const int NT = NP >> 5;
+    const int D = H * HD;
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nstrips = (q_rows + 31) >> 5;
+    const int nlast = (N - 1) >> 5;
+    const bool w16 = wid == nlast && wid < nstrips && N - 32 * nlast <= 16;
+    const bool active = wid < nstrips;
+    const int S = active ? 4 : 0;          // output store instructions per unit of this wave
+    const int G = gridDim.x;
+    const int J = ((int)blockIdx.x < BH) ? (BH - 1 - (int)blockIdx.x) / G + 1 : 0;   // units of this workgroup
+    if (J == 0) return;                    // workgroup-uniform
+    const int Gtot = J * NT;
+    const int nfull = N >> 5;
+    char* qarea = ring + R * 8192 + wid * 4096;   // this wave's query strip (K-image layout, rows = strip rows)
+    auto unit_base = [&](int j) -> const bf16_t* {
+        const int bh = (int)blockIdx.x + j * G;
+        const int b = bh / H, h = bh - (bh / H) * H;
+        return qkv + (int64_t)b * N * 3 * D + h * HD;
+    };
+    // lane-derived addresses are recomputed where they are used (lane_id_opaque: not hoistable), so nothing of the
+    // DMA / Q / store address math stays live across the key steps
+    const bool isv = wid >= 4;
+    auto issue = [&](int g) {   // this wave's piece of chunk g (clamped past the end) into slot g % R
+        const int ln = lane_id_opaque();
+        const int sub = ln >> 3, pslot = ln & 7;
+        const int gc = min(g, Gtot - 1);
+        const int j = gc / NT, c = gc - (gc / NT) * NT;
+        const int rl = 8 * (wid & 3) + sub;            // local row in the chunk
+        const int ch = isv ? (pslot ^ (((rl >> 1) & 1) << 2)) : (pslot ^ ((rl >> 1) & 7));
+        const bf16_t* src = unit_base(j) + (isv ? 2 * D : D) + (int64_t)min(c * 32 + rl, N - 1) * 3 * D + ch * 8;
+        char* dst = ring + (g % R) * 8192 + (isv ? 4096 : 0) + (wid & 3) * 1024;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+    };
+    auto issue_q = [&](int j) {   // the four 8-row pieces of this wave's query strip of unit min(j, J - 1)
+        const int ln = lane_id_opaque();
+        const int sub = ln >> 3, pslot = ln & 7;
+        const bf16_t* qb = unit_base(min(j, J - 1));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int rl = 8 * i + sub;
+            const int ch = pslot ^ ((rl >> 1) & 7);
+            __builtin_amdgcn_global_load_lds((gptr_t)(qb + (int64_t)min(wid * 32 + rl, N - 1) * 3 * D + ch * 8),
+                                             (lptr_t)(qarea + i * 1024), 16, 0, 0);
+        }
+    };
+    // ops issued after the piece of chunk s CB + CB - 1, at group top s (tools/sim/attn_ring_counts.py k_gt)
+    auto k_gt = [&](int s) {
+        const int gl = s * CB + CB - 1;
+        const int si = max(0, (gl - R + CB) / CB);
+        const int a = si * CB, b = s * CB;
+        const int nq = b > a ? (b - 1) / NT - (a == 0 ? -1 : (a - 1) / NT) : 0;   // unit starts in [a, b)
+        const int ns = b / NT - a / NT;                                             // unit ends in (a, b]
+        return (R - 2 * CB) + 4 * nq + S * ns;
+    };
+    // ops issued after the last Q(j) piece, at unit j's start (k_qw)
+    auto k_qw = [&](int j) { return j == 0 ? R : CB * ((j * NT) / CB - ((j - 1) * NT) / CB) + S; };
+    bf16x8 qf[4];
+    auto run = [&](auto k16) {
+        constexpr bool W16 = decltype(k16)::value;
+        issue_q(0);
+        for (int g = 0; g < R - CB; ++g) issue(g);
+        f32x16 o0 = {}, o1 = {};
+        f32x4 o16[4] = {};
+        float m = -INFINITY, l = 0.f;
+        for (int j = 0; j < J; ++j) {
+            if constexpr (W16) {
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt) o16[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            } else {
+                o0 = f32x16{};
+                o1 = f32x16{};
+            }
+            m = -INFINITY;
+            l = 0.f;
+            for (int c = 0; c < NT; ++c) {
+                const int g = j * NT + c;
+                if (g % CB == 0) {
+                    wait_vmcnt(k_gt(g / CB));
+                    __builtin_amdgcn_s_barrier();
+                    asm volatile("" ::: "memory");
+#pragma unroll
+                    for (int i = 0; i < CB; ++i) issue(g + R - CB + i);   // into the slots of group s - 1
+                }
+                if (c == 0) {
+                    // Q(j) from this wave's LDS area into registers, then Q(j + 1)'s DMA into the area (after the reads
+                    // have completed: lgkmcnt(0))
+                    wait_vmcnt(k_qw(j));
+                    asm volatile("" ::: "memory");
+                    {
+                        const int ln = lane_id_opaque();
+                        if constexpr (W16) {
+                            const int r16 = ln & 15, g4 = ln >> 4;
+#pragma unroll
+                            for (int kk = 0; kk < 4; ++kk)
+                                qf[kk] = *reinterpret_cast<const bf16x8*>(qarea + k_off(r16, 4 * (kk & 1) + g4));
+                        } else {
+                            const int l32 = ln & 31, hh = ln >> 5;
+#pragma unroll
+                            for (int ks = 0; ks < 4; ++ks)
+                                qf[ks] = *reinterpret_cast<const bf16x8*>(qarea + k_off(l32, ks * 2 + hh));
+                        }
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
+                    issue_q(j + 1);
+                }
+                if (!active) continue;
+                // slot of chunk g, addressed with the global key base kb (the swizzles depend on key mod 32 only)
+                const int kb = c * 32;
+                const char* Ks = ring + (g % R) * 8192 - kb * ROWB;
+                const char* Vs = Ks + 4096;
+                // the lane id re-read per step: the steps' lane-derived LDS addresses are then computed in the step,
+                // not hoisted out of both loops (which held ~10 VGPRs across them and spilled at the 128 limit)
+                const int lane = lane_id_opaque();
+                if (c < nfull) {
+                    if constexpr (W16) attn_step16<false>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o16);
+                    else attn_step<1, false, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+                } else {
+                    if constexpr (W16) attn_step16<true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o16);
+                    else if (N - kb <= 8) attn_step_tail8(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+                    else attn_step<1, true, true, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
+                }
+            }
+            // unit j's output rows (the pipe kernel's epilogues): S store instructions
+            if (active) {
+                const int ln = lane_id_opaque();
+                const int bh = (int)blockIdx.x + j * G;
+                const int b = bh / H, h = bh - (bh / H) * H;
+                const int64_t row0 = (int64_t)b * N;
+                if constexpr (W16) {
+                    l = xor32_sum(xor16_sum(l));
+                    const float inv = 1.0f / l;
+                    const int qq = wid * 32 + (ln & 15);
+                    bf16_t* orow = out + (row0 + min(qq, N - 1)) * D + h * HD + 4 * (ln >> 4);
+                    if (qq < q_rows) {
+#pragma unroll
+                        for (int dt = 0; dt < 4; ++dt)
+                            *reinterpret_cast<uint2*>(orow + 16 * dt) =
+                                make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
+                                           pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
+                    }
+                } else {
+                    const int q = wid * 32 + (ln & 31), hh = ln >> 5;
+                    l = xor32_sum(l);
+                    const float inv = 1.0f / l;
+                    uint32_t gx[8], gy[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const f32x16& o = k < 4 ? o0 : o1;
+                        const int b4 = 4 * (k & 3);
+                        gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
+                        gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
+                    }
+                    uint4 ov[4];
+#pragma unroll
+                    for (int k = 0; k < 8; k += 2) {
+                        const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
+                        const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
+                        ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+                    }
+                    bf16_t* orow = out + (row0 + min(q, N - 1)) * D + h * HD + 8 * hh;
+                    if (q < q_rows) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
+                    }
+                }
+            }
+        }
+    };
+    if (w16) run(std::true_type{});
+    else run(std::false_type{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may outlive the workgroup
+}
+
 // CLS-only attention (q_rows == 1: the last encoder block, whose other query rows feed nothing): one wave
 // per (particle, head), 4 per workgroup, no LDS, so occupancy is set by VGPRs and many heads stream K / V
 // at once (the path is pure HBM streaming: 2 x N x 128 B per head for one query).
@@ -977,6 +1179,25 @@ static int cu_count() {
     return cached;
 }
 
+static int attn_cus() {   // compute units of the current device (the persistent kernel's grid)
+    static int cached = 0;
+    if (!cached) {
+        int dev = 0, n = 0;
+        cached = (hipGetDevice(&dev) == hipSuccess &&
+                  hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) ? n : 256;
+    }
+    return cached;
+}
+// Attention kernel choice for N <= 256: 0 = k_attn_bf16_ring<2, 6>, 1 = the one-unit key-pipelined kernel, 2-3 = ring
+// variants (CB, R) = (3, 6), (1, 6). Process state set by an explicit call (tests,
+// A/B), never read from the environment.
+static int g_attn_variant = 1;
+VPF_API int vpf_attention_tune(int variant) {
+    if (variant < 0 || variant > 3) return VPF_ERR_ARG;
+    g_attn_variant = variant;
+    return 0;
+}
+
 VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, int N, int H, int hd, float scale,
                                int q_rows, void* stream) {
     if (B < 0 || N <= 0 || N > 640 || H <= 0 || hd != HD || B * H > INT32_MAX || q_rows < 1 || q_rows > N)
@@ -990,6 +1211,17 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     if (q_rows == 1) {
         hipLaunchKernelGGL(k_attn_cls_bf16, dim3((unsigned)((BH + 3) / 4)), dim3(256), 0, (hipStream_t)stream, qkv, out,
                            N, H, (int)BH, scale_log2);
+        VPF_RETURN_LAUNCH();
+    }
+    if (N <= 256 && g_attn_variant != 1) {   // round 4: the persistent chunk-ring kernel (vpf_attention_tune 0 / 2 / 3)
+        const int64_t BH = B * H;
+        const unsigned G = (unsigned)std::min<int64_t>(BH, 2 * (int64_t)attn_cus());
+        typedef void (*ring_fn)(const bf16_t*, bf16_t*, int, int, int, float, int);
+        ring_fn fn = k_attn_bf16_ring<2, 6>;
+        if (g_attn_variant == 2) fn = k_attn_bf16_ring<3, 6>;
+        if (g_attn_variant == 3) fn = k_attn_bf16_ring<1, 6>;
+        hipLaunchKernelGGL(fn, dim3(G), dim3(512), 0, (hipStream_t)stream, qkv, reinterpret_cast<bf16_t*>(out), N, H,
+                           (int)BH, scale_log2, q_rows);
         VPF_RETURN_LAUNCH();
     }
     // N <= 256: the key-pipelined kernel (8 waves, one strip each). VPF_ATTN_MODE=0 selects the

@@ -26,33 +26,28 @@ __device__ __forceinline__ int mx8_block_exp(uint32_t amax_bf16) {   // amax as 
     return min(max(E, -127), 125);
 }
 
-// |x| max of 8 packed bf16 values, as |bf16| bits (integer order = magnitude order): sign bits cleared on both halves,
-// packed 16-bit maxima (v_pk_max_u16), then the two halves (8 VALU instead of 13)
-typedef unsigned short vpf_u16x2 __attribute__((ext_vector_type(2)));
+// |x| max of 8 packed bf16 values, as |bf16| bits (integer order = magnitude order)
 __device__ __forceinline__ uint32_t mx8_amax8(uint4 v) {
-    const vpf_u16x2 a = __builtin_bit_cast(vpf_u16x2, v.x & 0x7fff7fffu), b = __builtin_bit_cast(vpf_u16x2, v.y & 0x7fff7fffu);
-    const vpf_u16x2 c = __builtin_bit_cast(vpf_u16x2, v.z & 0x7fff7fffu), d = __builtin_bit_cast(vpf_u16x2, v.w & 0x7fff7fffu);
-    const vpf_u16x2 m = __builtin_elementwise_max(__builtin_elementwise_max(a, b), __builtin_elementwise_max(c, d));
-    return max((uint32_t)m.x, (uint32_t)m.y);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t am = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) am = max(am, max(w[e] & 0x7fffu, (w[e] >> 16) & 0x7fffu));
+    return am;
 }
 
-// 8 packed bf16 values -> 8 e4m3 bytes of RNE(x * 2^-E) (E = the block exponent), by gfx950's
-// v_cvt_scalef32_pk_fp8_bf16: the packed bf16 pair converted with the block scale in one instruction (4 per 8 values
-// instead of 8 unpacks + 8 multiplies + 4 v_cvt_pk_fp8_f32). The instruction divides by its scale operand: with scale
-// 2^E it is bit-identical to RNE(x * 2^-E) for every E in [-127, 125] (tools/micro/cvt_scalef.py on the MI355X: 0 of
-// 1,048,576 pairs differ; with 2^-E 98.9 % of them differ: profiles/r4_lab/cvt_scalef_probe.txt).
-typedef __bf16 vpf_bf16x2 __attribute__((ext_vector_type(2)));
-typedef short vpf_s16x2 __attribute__((ext_vector_type(2)));
+// 8 packed bf16 values -> 8 e4m3 bytes of x * 2^-E (E = the block exponent)
 __device__ __forceinline__ uint2 mx8_pack8(uint4 v, int E) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    const float sc = __uint_as_float((uint32_t)(127 + E) << 23);      // 2^E (normal for E in [-127, 125])
-    vpf_s16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(vpf_s16x2{0, 0}, __builtin_bit_cast(vpf_bf16x2, w[0]), sc,
-                                                             false);
-    lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(lo, __builtin_bit_cast(vpf_bf16x2, w[1]), sc, true);
-    vpf_s16x2 hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(vpf_s16x2{0, 0}, __builtin_bit_cast(vpf_bf16x2, w[2]), sc,
-                                                             false);
-    hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(hi, __builtin_bit_cast(vpf_bf16x2, w[3]), sc, true);
-    return make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+    const float inv = __uint_as_float((uint32_t)(127 - E) << 23);     // 2^-E (normal for E in [-127, 125])
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)(w[0] & 0xffff)) * inv, bf2f((bf16_t)(w[0] >> 16)) * inv, 0,
+                                             false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)(w[1] & 0xffff)) * inv, bf2f((bf16_t)(w[1] >> 16)) * inv, lo,
+                                         true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)(w[2] & 0xffff)) * inv, bf2f((bf16_t)(w[2] >> 16)) * inv, 0,
+                                             false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)(w[3] & 0xffff)) * inv, bf2f((bf16_t)(w[3] >> 16)) * inv, hi,
+                                         true);
+    return make_uint2((uint32_t)lo, (uint32_t)hi);
 }
 
 // 8 consecutive bf16 values of one row (one lane) -> 8 e4m3 bytes; the 32-value block is the lane's DPP quad

@@ -48,7 +48,6 @@ SIGNATURES = {
     "vpf_quantize_mx8": [_P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _P],
     "vpf_gemm_bf16_splitk": [_P, _I64, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I32, _I32, _P, _P, _I64, _P],
     "vpf_gemm_tune": [_I32, _I32],
-    "vpf_attention_tune": [_I32],
     "vpf_gemm_f32": [_P, _I64, _P, _P, _P, _P, _I32, _P, _P, _P, _I64, _I64, _I64, _I64, _I32, _P],
     "vpf_row_stats_bf16": [_P, _I64, _I32, _I64, _F32, _P, _P],
     "vpf_row_stats_f32": [_P, _I64, _I32, _I64, _F32, _P, _P],
