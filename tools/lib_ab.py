@@ -89,8 +89,12 @@ def main():
         for k, L in (("product", P), ("other", O)):
             assert (call(L, k, reset=True) if case.startswith("mx8") else call(L, k)) == 0, (case, k)
         torch.cuda.synchronize()
-        def snap(k):
+        def snap(k):   # the outputs the call writes
             b = bufs[k]
+            if case == "mx8_fc1":
+                b = b[1:3]
+            elif case == "mx8_qkv":
+                b = b[:1]
             return [t.clone() for t in (b if isinstance(b, (tuple, list)) else (b,)) if t is not None]
         same = all(torch.equal(x, y) for x, y in zip(snap("product"), snap("other")))
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
