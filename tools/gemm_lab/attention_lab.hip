@@ -830,7 +830,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 //    CB, the wave's store count) checked against a simulation of the issue sequence (tools/sim/attn_ring_counts.py).
 //  * Per query row the arithmetic is the one-unit kernel's (same step functions, same order): bit-identical output.
 // N <= 256 (one strip per wave), bf16 output.
-template <int CB, int R>
+// LABR (round 4 split of the ring's time): 1 = loads, waits and barriers only (no key steps), 2 = compute only (no K / V
+// DMA: the steps read whatever the ring holds; the counted waits then retire nothing but Q)
+template <int CB, int R, int LABR = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16_ring(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, int BH, float scale_log2, int q_rows) {
     static_assert(R >= 2 * CB, "the ring holds the group being computed and the group in flight");
@@ -868,7 +870,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         const int ch = isv ? (pslot ^ (((rl >> 1) & 1) << 2)) : (pslot ^ ((rl >> 1) & 7));
         const bf16_t* src = unit_base(j) + (isv ? 2 * D : D) + (int64_t)min(c * 32 + rl, N - 1) * 3 * D + ch * 8;
         char* dst = ring + (g % R) * 8192 + (isv ? 4096 : 0) + (wid & 3) * 1024;
-        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+        if constexpr (LABR != 2) __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
     };
     auto issue_q = [&](int j) {   // the four 8-row pieces of this wave's query strip of unit min(j, J - 1)
         const int ln = lane_id_opaque();
@@ -942,7 +944,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
                     issue_q(j + 1);
                 }
-                if (!active) continue;
+                if (!active || LABR == 1) continue;
                 // slot of chunk g, addressed with the global key base kb (the swizzles depend on key mod 32 only)
                 const int kb = c * 32;
                 const char* Ks = ring + (g % R) * 8192 - kb * ROWB;
@@ -1193,7 +1195,7 @@ static int attn_cus() {   // compute units of the current device (the persistent
 // A/B), never read from the environment.
 static int g_attn_variant = 1;
 VPF_API int vpf_attention_tune(int variant) {
-    if (variant < 0 || variant > 3) return VPF_ERR_ARG;
+    if (variant < 0 || variant > 5) return VPF_ERR_ARG;
     g_attn_variant = variant;
     return 0;
 }
@@ -1219,6 +1221,8 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
         typedef void (*ring_fn)(const bf16_t*, bf16_t*, int, int, int, float, int);
         ring_fn fn = k_attn_bf16_ring<2, 6>;
         if (g_attn_variant == 2) fn = k_attn_bf16_ring<3, 6>;
+        if (g_attn_variant == 4) fn = k_attn_bf16_ring<3, 6, 1>;
+        if (g_attn_variant == 5) fn = k_attn_bf16_ring<3, 6, 2>;
         if (g_attn_variant == 3) fn = k_attn_bf16_ring<1, 6>;
         hipLaunchKernelGGL(fn, dim3(G), dim3(512), 0, (hipStream_t)stream, qkv, reinterpret_cast<bf16_t*>(out), N, H,
                            (int)BH, scale_log2, q_rows);
