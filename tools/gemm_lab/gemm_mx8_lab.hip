@@ -56,7 +56,9 @@ __device__ __forceinline__ void mx_row(f32x4 (&acc)[4][8], const i32x8 (&b)[4], 
 
 // LAB (lab builds only, VPF_MX8_VARIANT 7 / 8 / 9): 1 = no epilogue (the K loop alone), 2 = the loop's DMAs and
 // barriers only, 3 = DMAs + fragment reads (no MFMAs): timing probes that do not write C. 4 (VPF_MX8_VARIANT=6) =
-// the row-major counted-wait schedule, full kernel.
+// the row-major counted-wait schedule, full kernel. Round 4 sync bounds of the loop alone (no epilogue, results
+// garbage): 6 (VPF_MX8_VARIANT=a) = the buffer-release barrier removed (one barrier per K-tile, the cost a three-stage
+// ring would pay), 7 (=b) = no barrier at all, each wave waits for its own DMA pieces only.
 template <int EPI, bool OUT8, bool EARLY = true, int LAB = 0>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict__ A, int lda,
                                                        const uint32_t* __restrict__ As, int lds_a,
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
     stage(1, min(1, nk - 1));
     for (int kt = 0; kt < nk; ++kt) {
         asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-        __builtin_amdgcn_s_barrier();   // K-tile kt (and the epilogue operands) landed for every wave
+        if constexpr (LAB != 7) __builtin_amdgcn_s_barrier();   // K-tile kt (and the epilogue operands) landed
         asm volatile("" ::: "memory");
         const char* st = smem + (kt & 1) * STAGE;
         const char* la = st;
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
             // the first column group's 8 MFMAs run before the buffer-release barrier (they need only registers),
             // so the MFMA pipe works while the slower waves finish their reads
             mx_col<0>(acc[0], b[0], a, sb, sa0, sa1);
-            __builtin_amdgcn_s_barrier();
+            if constexpr (LAB != 6 && LAB != 7) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             stage(kt & 1, min(kt + 2, nk - 1));
             mx_col<1>(acc[1], b[1], a, sb, sa0, sa1);
@@ -302,7 +304,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
         __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing refills land before the ring is reused
-    if constexpr (LAB >= 1 && LAB <= 3) {
+    if constexpr ((LAB >= 1 && LAB <= 3) || LAB >= 6) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -380,7 +382,9 @@ __global__ __launch_bounds__(256) void k_quantize_mx8(const bf16_t* __restrict__
         if (labv == 4 && o8.q) { hipLaunchKernelGGL((k_gemm_mx8<E, true, true, 4>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
         if (labv == 4) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 4>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
         if (labv == 5 && o8.q) { hipLaunchKernelGGL((k_gemm_mx8<E, true, true, 5>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
-        if (labv == 5) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 5>), grid, block, 0, s, VPF_MX8_ARGS); break; }
+        if (labv == 5) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 5>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 6) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 6>), grid, block, 0, s, VPF_MX8_ARGS); break; } \
+        if (labv == 7) { hipLaunchKernelGGL((k_gemm_mx8<E, false, true, 7>), grid, block, 0, s, VPF_MX8_ARGS); break; }
 #else
 #define VPF_MX8_LAB_LAUNCH(E)
 #endif
@@ -427,7 +431,8 @@ VPF_API int vpf_gemm_mx8(const uint8_t* A, int64_t lda, const uint32_t* As, int6
     const bool late = var && var[0] == '0';
     // lab builds: 7 / 8 / 9 -> LAB 1 / 2 / 3 (probes), 6 -> LAB 4 (row-major schedule, full kernel)
     const int labv = var && var[0] >= '7' && var[0] <= '9' ? var[0] - '6' : var && var[0] == '6' ? 4
-                     : var && var[0] == '5' ? 5 : 0;   // 5 -> LAB 5: the pipelined fp8-only epilogue
+                     : var && var[0] == '5' ? 5 : var && var[0] == 'a' ? 6 : var && var[0] == 'b' ? 7
+                     : 0;   // 5 -> LAB 5: the pipelined fp8-only epilogue; a / b -> LAB 6 / 7 (round-4 sync bounds)
     (void)labv;
     switch (epilogue) {
         case VPF_EPI_BIAS: VPF_MX8_LAUNCH(VPF_EPI_BIAS); break;
