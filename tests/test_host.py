@@ -223,3 +223,50 @@ def test_weights_digest_tracks_the_weight_set():
     w["blocks.3.mlp.fc1.bias"] = w["blocks.3.mlp.fc1.bias"].clone()
     w["blocks.3.mlp.fc1.bias"][7] += 1e-3
     assert weights_digest(w) != d0
+
+
+def _vregs(tok):
+    m = re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.fullmatch(r"v(\d+)", tok)
+    return {int(m.group(1))} if m else set()
+
+
+def test_attention_q_loads_are_waited_before_any_use(tmp_path):
+    """ADVICE r3 (Q-load asm safety), checked on the compiled code instead of trusted: the key-pipelined attention
+    loads its Q fragments with inline-asm global_load_dwordx4 (hipcc must not count them, or it drains the K / V
+    DMAs with them), so nothing but the kernel's own shape orders them before their uses. Rounds 2 and 4 each broke
+    that shape once (a phi of asm outputs: register copies of not-yet-landed loads, NaNs on the GPU). Here the device
+    code of csrc/attention.hip is compiled to gfx950 assembly and, for both k_attn_bf16_pipe instances:
+    * the Q loads are exactly four asm global_load_dwordx4 into VGPRs;
+    * between the last of them and the empty pin asm that follows the counted wait, there is at least one
+      `s_waitcnt vmcnt` and no instruction names any VGPR those loads write (no copy, no read, no reuse)."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(ROOT, "vitparticlefiltertracker_amd", "csrc", "attention.hip")
+    out = tmp_path / "attention.s"
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-function", "--cuda-device-only",
+                    "-S", "-o", str(out), src], check=True, capture_output=True)
+    funcs = re.split(r"\n(?=_Z\S*:)", out.read_text())
+    checked = 0
+    for f in funcs:
+        name = f.split(":", 1)[0]
+        if "k_attn_bf16_pipe" not in name:
+            continue
+        L = [ln.strip() for ln in f.splitlines()]
+        loads = [(i, _vregs(ln.split()[1].rstrip(","))) for i, ln in enumerate(L)
+                 if ln.startswith("global_load_dwordx4 v[") and L[i - 1] == ";;#ASMSTART"]
+        assert len(loads) == 4, (name, loads)
+        last = loads[-1][0]
+        pin = next(i for i in range(last + 1, len(L) - 1) if L[i] == ";;#ASMSTART" and L[i + 1] == ";;#ASMEND")
+        assert any(L[i].startswith("s_waitcnt") and "vmcnt" in L[i] for i in range(last, pin)), name
+        qregs = set().union(*(r for _, r in loads))
+        touched = [L[i] for i in range(last + 1, pin)
+                   if any(_vregs(t) & qregs for t in re.findall(r"v\[\d+:\d+\]|\bv\d+\b", L[i]))]
+        assert not touched, (name, touched[:4])
+        checked += 1
+    assert checked == 2, checked
