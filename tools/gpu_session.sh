@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU session: each GPU step under its own time limit; stop at the first crash / timeout / abort.
-# Usage: tools/gpu_session.sh <tag> [host] [tests] [scale] [smoke] [bench] [bench_l] [bench8] [prof] [pmc] [pmc8]
+# Usage: tools/gpu_session.sh <tag> [host] [tests] [scale] [smoke] [bench] [bench_l] [bench8] [prof] [pmc] [pmcmfma] [pmc8]
 #        [pfprobe] [cpuframe] [lab]
 #   env: PYTEST_K (pytest -k filter for "tests"), LAB_SHAPES / LAB_VARS (gemm_lab filters)
 TAG=$1; shift
@@ -61,6 +61,12 @@ for step in "$@"; do
       ok_or_stop $? pmc_write
       python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write > $OUT/pmc_traffic.json 2> $OUT/pmc_traffic.err
       ok_or_stop $? pmc_traffic; cat $OUT/pmc_traffic.json | head -40 ;;
+    pmcmfma)   # MFMA-busy and clock of every kernel of the bench frame (one pass: 2 SQ + 1 GRBM counters)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_mfma -o p --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc_mfma.log 2>&1
+      ok_or_stop $? pmc_mfma
+      python tools/pmc_frame.py $OUT/pmc_mfma --frames 3 > $OUT/pmc_mfma_frame.txt 2>&1
+      ok_or_stop $? pmc_frame; cat $OUT/pmc_mfma_frame.txt ;;
     pmc8)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc8_fetch -o p --output-format csv -- python3 bench.py --dtype fp8 --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc8_fetch.log 2>&1
