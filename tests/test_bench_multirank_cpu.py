@@ -101,3 +101,14 @@ def test_multi_rank_check_detects_disagreement(fault, flag):
     out = _run(2, 64, fault)
     for r, res in out.items():                             # every rank reaches the same verdict
         assert not res["ok"] and not res[flag], (r, res)
+
+
+def test_cpu_full_frame_measures_or_falls_back_within_budget():
+    """bench.py's cpu_baseline: a measured full oracle frame, or, when a 32-crop probe projects the frame past
+    --cpu-frame-budget, the bounded sample marked as such (never an unmarked extrapolation)."""
+    import bench
+    full = bench.cpu_full_frame("vit_tiny_patch16_224", 48, 2, 0.0, budget_s=480.0)
+    assert full["measured"] == "full frame" and full["s_per_frame"] > 0 and full["cores"] == 2
+    assert abs(full["value"] * full["s_per_frame"] - 1.0) < 0.02
+    fb = bench.cpu_full_frame("vit_tiny_patch16_224", 48, 2, 1.0, budget_s=1e-6)
+    assert fb["measured"].startswith("bounded sample") and fb["s_per_frame"] > 0 and fb["kind"] == "port"
