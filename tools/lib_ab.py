@@ -4,7 +4,8 @@ the lab build, tools/gemm_lab -> libvpf_lab.so, whose MX8 GEMM / attention are t
 same device buffers; interleaved rounds, HIP-event medians, outputs compared bit for bit.
 
 Cases: mx8_fc1 (LN + GELU, MX8-only output: FC2's A operand), mx8_fc2 (residual + planes + the MX8 copy of h),
-mx8_qkv (LN fold, bf16 out), quant (vpf_quantize_mx8 of a bf16 [M][768] tensor), attn (bf16 attention, N = 197).
+mx8_qkv (LN fold, bf16 out), quant (vpf_quantize_mx8 of a bf16 [M][768] tensor), attn (bf16 attention, N = 197),
+attn577 (bf16 attention at ViT-L/14 @ 336's N = 577, 16 heads).
 
 usage: python tools/lib_ab.py [rounds] [cases] [other_lib]      env AB_M (rows, default 4096*197)
 """
@@ -39,8 +40,11 @@ def main():
     pt = E.ptr
     for case in cases:
         outs = {}
-        if case == "attn":
-            B, N, H = M // 197, 197, 12
+        if case in ("attn", "attn577"):
+            # attn: ViT-B/16 @ 224 (N = 197, 12 heads, the key-pipelined kernel); attn577: ViT-L/14 @ 336 (N = 577,
+            # 16 heads, the whole-image kernel), 4096 particles unless AB_M says otherwise
+            N, H = (197, 12) if case == "attn" else (577, 16)
+            B = M // 197
             qkv = (torch.randn(B, N, 3 * 64 * H, device=dev, generator=g) * 1.5).to(torch.bfloat16)
             bufs = {k: torch.empty(B, N, 64 * H, device=dev, dtype=torch.bfloat16) for k in ("product", "other")}
 
