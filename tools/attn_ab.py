@@ -1,9 +1,10 @@
 """Same-process A/B of the bf16 attention launch variants at the configs[1] shape (4096 particles x 12 heads, N = 197):
 rounds of (variant A, variant B, ...) launches, HIP-event time per launch, medians per variant.
 
-Variants: "tune=<k>" = vpf_attention_tune(k) of the product library (0 = the persistent chunk ring, 1 = the one-unit
-key-pipelined kernel, 2 / 3 = other ring geometries); anything else is a set of environment settings for the lab library
-(VPF_LIB_PATH=.../libvpf_lab.so: VPF_ATTN_TAIL16, VPF_ATTN_TAIL, VPF_ATTN_MODE, VPF_ATTN_LAB).
+Lab library only (VPF_LIB_PATH=vitparticlefiltertracker_amd/libvpf_lab.so: the product library has no variants).
+Variants: "tune=<k>" = its vpf_attention_tune(k) (0 = the persistent chunk ring, 1 = the one-unit key-pipelined kernel,
+2 / 3 = other ring geometries, 4 / 5 = the ring's load-only / compute-only probes); anything else is a set of
+environment settings the lab library reads (VPF_ATTN_TAIL16, VPF_ATTN_TAIL, VPF_ATTN_MODE, VPF_ATTN_LAB).
 
     python tools/attn_ab.py [--particles 4096] [--rounds 15] [--n 197] [tune=1 tune=0 ...]
 """
