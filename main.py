@@ -1,6 +1,10 @@
 """`python main.py [--config config.yaml]` — the entry point the reference documents (README.md:34-38):
 read the config, feed frames to the Tracker, print the tracked positions (README.md:42).
 
+Several targets (README.md:46-50, SPEC S9): `input.bboxes: [[x, y, w, h], ...]` runs a MultiTracker (one batched ViT
+pass over every target's particles); each frame then prints and records one position per target, and --video-out
+draws every box. Checkpoint / resume covers the single-target Tracker.
+
 Multi-GPU: `torchrun --nproc-per-node G --master-addr 127.0.0.1 main.py` shards the particles over G GPUs.
 """
 from __future__ import annotations
@@ -29,7 +33,7 @@ def main(argv=None) -> int:
 
     import torch
     import torch.distributed as dist
-    from vitparticlefiltertracker_amd import Tracker, load_config
+    from vitparticlefiltertracker_amd import MultiTracker, Tracker, load_config
     from vitparticlefiltertracker_amd.frames import (Y4MWriter, draw_box, iter_frames, prefetch, synthetic_clip,
                                                       write_ppm)
 
@@ -46,6 +50,11 @@ def main(argv=None) -> int:
     else:
         src = itertools.islice(iter_frames(inp["source"]), n)
     frames = prefetch(src, depth=2)   # decode + pin on a host thread, overlapped with the GPU frame loop
+    boxes = inp.get("bboxes")
+    if boxes is not None:
+        if args.checkpoint or args.resume:
+            raise SystemExit("--checkpoint / --resume cover the single-target Tracker (input.bboxes is set)")
+        return _run_multi(args, cfg, boxes, frames, MultiTracker, dist)
     tr = Tracker(cfg)
     first = next(frames)
     start = 1
@@ -98,6 +107,63 @@ def main(argv=None) -> int:
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0
+
+
+def _sink(args, rank):
+    """(emit(k, rgb, boxes), close()) for --video-out: the frame with every box drawn, as .y4m or PPM frames."""
+    from vitparticlefiltertracker_amd.frames import Y4MWriter, draw_box, write_ppm
+    if not args.video_out or rank != 0:
+        return (lambda k, rgb, boxes: None), (lambda: None)
+    writer = Y4MWriter(args.video_out) if args.video_out.lower().endswith(".y4m") else None
+    if writer is None:
+        os.makedirs(args.video_out, exist_ok=True)
+
+    def emit(k, rgb, boxes):
+        img = rgb.numpy() if hasattr(rgb, "numpy") else rgb
+        for b in boxes:
+            img = draw_box(img, b)
+        if writer is not None:
+            writer.write(img)
+        else:
+            write_ppm(os.path.join(args.video_out, f"frame_{k:05d}.ppm"), img)
+    return emit, (writer.close if writer is not None else (lambda: None))
+
+
+def _run_multi(args, cfg, boxes, frames, MultiTracker, dist) -> int:
+    """input.bboxes: K targets tracked by one MultiTracker; one line and one JSON record per frame with every
+    target's (x, y, scale)."""
+    mt = MultiTracker(cfg, n_objects=len(boxes))
+    first = next(frames)
+    mt.init(first, boxes)
+    emit, close = _sink(args, mt.rank)
+    emit(0, first, boxes)
+    t0 = time.perf_counter()
+    out = []
+    for k, f in enumerate(frames, start=1):
+        ests = mt.track(f)
+        out.append({"frame": k, "targets": [{"x": x, "y": y, "scale": s} for x, y, s in ests]})
+        emit(k, f, [_box(st, b) for st, b in zip(ests, boxes)])
+        if mt.rank == 0:
+            print(f"frame {k:4d}  " + "  ".join(f"[{i}] x={x:8.2f} y={y:8.2f} s={s:6.3f}"
+                                                 for i, (x, y, s) in enumerate(ests)), flush=True)
+    close()
+    dt = time.perf_counter() - t0
+    if mt.rank == 0:
+        print(f"{len(out)} frames x {len(boxes)} targets in {dt:.3f} s ({len(out) / max(dt, 1e-9):.2f} frames/s)",
+              file=sys.stderr)
+        if args.out:
+            with open(args.out, "w") as fh:
+                json.dump(out, fh, indent=1)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
+def _box(state, bbox0):
+    """(x, y, w, h) of a state (centre, scale) for a target whose frame-0 box is bbox0 (SPEC S3)."""
+    x, y, s = (float(v) for v in state)
+    w, h = s * float(bbox0[2]), s * float(bbox0[3])
+    return x - 0.5 * w, y - 0.5 * h, w, h
 
 
 if __name__ == "__main__":

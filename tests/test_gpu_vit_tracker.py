@@ -243,6 +243,38 @@ def test_main_video_out(tmp_path):
     assert red.sum() > 100                          # the box outline is there
 
 
+def test_main_multi_object(tmp_path):
+    """main.py with input.bboxes (README.md:46-50, SPEC S9): one MultiTracker over two targets; the JSON has one record
+    per frame with both targets, target 0's track is main.py's single-target track bit for bit (the batched pass is
+    row-independent and target 0 keeps particles.seed), and --video-out draws both boxes."""
+    import json
+    import sys
+    import yaml
+    from vitparticlefiltertracker_amd.frames import read_pnm
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+    import main as vpf_main
+    base = {"model": {"arch": "vit_tiny_patch16_224", "dtype": "bf16"}, "particles": {"num": 128, "seed": 3},
+            "input": {"source": "synthetic", "frames": 4, "bbox0": [80, 80, 64, 64]}}
+    one, two = tmp_path / "one.yaml", tmp_path / "two.yaml"
+    one.write_text(yaml.safe_dump(base))
+    multi = {**base, "input": {**base["input"], "bboxes": [[80, 80, 64, 64], [20, 140, 48, 40]]}}
+    two.write_text(yaml.safe_dump(multi))
+    o1, o2, vid = tmp_path / "one.json", tmp_path / "two.json", tmp_path / "frames"
+    assert vpf_main.main(["--config", str(one), "--out", str(o1)]) == 0
+    assert vpf_main.main(["--config", str(two), "--out", str(o2), "--video-out", str(vid)]) == 0
+    r1, r2 = json.loads(o1.read_text()), json.loads(o2.read_text())
+    assert [r["frame"] for r in r2] == [1, 2, 3] and all(len(r["targets"]) == 2 for r in r2)
+    for a, b in zip(r1, r2):
+        assert (a["x"], a["y"], a["scale"]) == (b["targets"][0]["x"], b["targets"][0]["y"], b["targets"][0]["scale"])
+    assert len(list(vid.glob("frame_*.ppm"))) == 4
+    f0 = read_pnm(vid / "frame_00000.ppm")            # lossless sink: the outlines are exact (255, 0, 0)
+    for x, y, w, h in multi["input"]["bboxes"]:
+        assert (f0[y, x:x + w] == (255, 0, 0)).all() and (f0[y:y + h, x] == (255, 0, 0)).all()
+        assert (f0[y + h - 1, x:x + w] == (255, 0, 0)).all() and (f0[y:y + h, x + w - 1] == (255, 0, 0)).all()
+    with pytest.raises(SystemExit):
+        vpf_main.main(["--config", str(two), "--checkpoint", str(tmp_path / "ck")])
+
+
 def test_multitracker_one_target_equals_tracker():
     """MultiTracker's batched pass is row-independent: with one target it reproduces Tracker bit for bit."""
     from vitparticlefiltertracker_amd import MultiTracker, Tracker

@@ -270,3 +270,14 @@ def test_attention_q_loads_are_waited_before_any_use(tmp_path):
         assert not touched, (name, touched[:4])
         checked += 1
     assert checked == 2, checked
+
+
+def test_config_bboxes_validation():
+    """input.bboxes (several targets, main.py -> MultiTracker): null by default, else a non-empty list of [x, y, w, h]
+    boxes with w, h > 0."""
+    assert C.load_config(None)["input"]["bboxes"] is None
+    c = C.load_config({"input": {"bboxes": [[1, 2, 30, 40], [5, 6, 7, 8]]}})
+    assert c["input"]["bboxes"] == [[1, 2, 30, 40], [5, 6, 7, 8]]
+    for bad in ([], [[1, 2, 3]], [[1, 2, 0, 4]], [[1, 2, 3, float("nan")]], "x"):
+        with pytest.raises(ValueError):
+            C.load_config({"input": {"bboxes": bad}})

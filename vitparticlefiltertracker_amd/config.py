@@ -102,7 +102,8 @@ DEFAULTS: Dict[str, Any] = {
                    "template_update": 0.0},     # alpha: t <- normalise((1 - alpha) t + alpha f(estimate)); 0 = fixed
     "resample": {"method": "systematic"},
     "input": {"source": "synthetic", "frames": 32, "height": 224, "width": 224,
-              "bbox0": [80, 80, 64, 64], "seed": 7},
+              "bbox0": [80, 80, 64, 64], "seed": 7,
+              "bboxes": None},                # several targets (SPEC S9): [[x, y, w, h], ...]; main.py -> MultiTracker
     "distributed": {"world_size": 1},
 }
 
@@ -141,6 +142,14 @@ def load_config(cfg: Optional[Any] = None) -> Dict[str, Any]:
         raise ValueError("likelihood.template_update must be in [0, 1]")
     if out["resample"]["method"] != "systematic":
         raise ValueError("only resample.method == 'systematic' is defined (SPEC S7)")
+    boxes = out["input"].get("bboxes")
+    if boxes is not None:
+        if not isinstance(boxes, (list, tuple)) or not boxes:
+            raise ValueError("input.bboxes must be a non-empty list of [x, y, w, h] boxes (or null)")
+        for b in boxes:
+            if not isinstance(b, (list, tuple)) or len(b) != 4 or not all(math.isfinite(float(v)) for v in b) \
+                    or float(b[2]) <= 0 or float(b[3]) <= 0:
+                raise ValueError(f"input.bboxes: {b!r} is not an [x, y, w, h] box with w, h > 0")
     return out
 
 
