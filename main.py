@@ -2,8 +2,8 @@
 read the config, feed frames to the Tracker, print the tracked positions (README.md:42).
 
 Several targets (README.md:46-50, SPEC S9): `input.bboxes: [[x, y, w, h], ...]` runs a MultiTracker (one batched ViT
-pass over every target's particles); each frame then prints and records one position per target, and --video-out
-draws every box. Checkpoint / resume covers the single-target Tracker.
+pass over every target's particles); each frame then prints and records one position per target, --video-out
+draws every box, and --checkpoint / --resume save and restore every target.
 
 Multi-GPU: `torchrun --nproc-per-node G --master-addr 127.0.0.1 main.py` shards the particles over G GPUs.
 """
@@ -52,8 +52,6 @@ def main(argv=None) -> int:
     frames = prefetch(src, depth=2)   # decode + pin on a host thread, overlapped with the GPU frame loop
     boxes = inp.get("bboxes")
     if boxes is not None:
-        if args.checkpoint or args.resume:
-            raise SystemExit("--checkpoint / --resume cover the single-target Tracker (input.bboxes is set)")
         return _run_multi(args, cfg, boxes, frames, MultiTracker, dist)
     tr = Tracker(cfg)
     first = next(frames)
@@ -134,18 +132,31 @@ def _run_multi(args, cfg, boxes, frames, MultiTracker, dist) -> int:
     target's (x, y, scale)."""
     mt = MultiTracker(cfg, n_objects=len(boxes))
     first = next(frames)
-    mt.init(first, boxes)
+    start = 1
+    if args.resume:
+        mt.load_checkpoint(args.resume)
+        for _ in range(mt.frame_index):       # frames 1 .. frame_index were tracked before the checkpoint
+            if next(frames, None) is None:
+                raise SystemExit(f"--resume: the checkpoint is at frame {mt.frame_index}, past the end of the input")
+        start = mt.frame_index + 1
+    else:
+        mt.init(first, boxes)
     emit, close = _sink(args, mt.rank)
-    emit(0, first, boxes)
+    if not args.resume:
+        emit(0, first, boxes)
     t0 = time.perf_counter()
     out = []
-    for k, f in enumerate(frames, start=1):
+    for k, f in enumerate(frames, start=start):
         ests = mt.track(f)
         out.append({"frame": k, "targets": [{"x": x, "y": y, "scale": s} for x, y, s in ests]})
         emit(k, f, [_box(st, b) for st, b in zip(ests, boxes)])
         if mt.rank == 0:
             print(f"frame {k:4d}  " + "  ".join(f"[{i}] x={x:8.2f} y={y:8.2f} s={s:6.3f}"
                                                  for i, (x, y, s) in enumerate(ests)), flush=True)
+        if args.checkpoint and args.checkpoint_every > 0 and k % args.checkpoint_every == 0:
+            mt.save_checkpoint(args.checkpoint)
+    if args.checkpoint:
+        mt.save_checkpoint(args.checkpoint)
     close()
     dt = time.perf_counter() - t0
     if mt.rank == 0:

@@ -271,8 +271,14 @@ def test_main_multi_object(tmp_path):
     for x, y, w, h in multi["input"]["bboxes"]:
         assert (f0[y, x:x + w] == (255, 0, 0)).all() and (f0[y:y + h, x] == (255, 0, 0)).all()
         assert (f0[y + h - 1, x:x + w] == (255, 0, 0)).all() and (f0[y:y + h, x + w - 1] == (255, 0, 0)).all()
-    with pytest.raises(SystemExit):
-        vpf_main.main(["--config", str(two), "--checkpoint", str(tmp_path / "ck")])
+    # checkpoint after frame 2, resume for frame 3: the same positions as the uninterrupted run, bit for bit
+    ck, o3 = tmp_path / "ck", tmp_path / "resumed.json"
+    assert vpf_main.main(["--config", str(two), "--frames", "3", "--checkpoint", str(ck)]) == 0
+    assert vpf_main.main(["--config", str(two), "--resume", str(ck) + ".npz", "--out", str(o3)]) == 0
+    assert json.loads(o3.read_text()) == r2[2:]
+    # a single-target tracker refuses a multi-target checkpoint
+    with pytest.raises(ValueError):
+        vpf_main.main(["--config", str(one), "--resume", str(ck) + ".npz"])
 
 
 def test_multitracker_one_target_equals_tracker():

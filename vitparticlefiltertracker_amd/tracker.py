@@ -39,6 +39,42 @@ def weights_digest(weights) -> str:
     return f"{crc:08x}"
 
 
+def _fingerprint(cfg, arch_name: str, digest: str, rank: int, world_size: int) -> dict:
+    """Every configuration value a tracking frame's arithmetic depends on: a checkpoint records these and
+    a resume under any other value is refused instead of drifting from the original run."""
+    m, p, lk = cfg["model"], cfg["particles"], cfg["likelihood"]
+    return {"arch": arch_name, "dtype": str(m["dtype"]), "weights_seed": int(m["weights"]["seed"]),
+            "weights_crc32": digest,
+            "mean": [float(v) for v in m["mean"]], "std": [float(v) for v in m["std"]],
+            "P": int(p["num"]), "motion_std": [float(v) for v in p["motion_std"]],
+            "scale_range": [float(v) for v in p["scale_range"]], "seed": int(p["seed"]),
+            "lambda": float(lk["lambda"]), "weight_bits": int(lk["weight_bits"]),
+            "template_update": float(lk["template_update"]), "rank": rank, "world_size": world_size}
+
+
+def _check_fingerprint(sd: dict, mine: dict) -> None:
+    import json
+    fmt = int(sd["format"])
+    if fmt == 1:
+        raise ValueError("checkpoint format 1 (rounds 1-2) records only P, rank, world size, seed and arch; format 2 "
+                         "also checks every value the tracking arithmetic depends on (dtype, lambda, motion, "
+                         "weights, ...): re-create the checkpoint with this version")
+    if fmt != 2:
+        raise ValueError(f"unknown checkpoint format {fmt}")
+    saved = json.loads(str(sd["config"]))
+    diff = sorted(k for k in set(saved) | set(mine) if saved.get(k) != mine.get(k))
+    if diff:
+        raise ValueError("checkpoint was written by a tracker with another configuration or rank layout: "
+                         + ", ".join(f"{k} {saved.get(k)!r} != {mine.get(k)!r}" for k in diff))
+
+
+def _checkpoint_file(path: str, rank: int, world_size: int) -> str:
+    """`<path>.rank<r>of<G>.npz` with several ranks, `<path>.npz` with one; a path that already names this rank's
+    file (what save_checkpoint returned) is taken as is, so save -> load round-trips either way."""
+    suffix = f".rank{rank}of{world_size}.npz" if world_size > 1 else ".npz"
+    return path if path.endswith(suffix) else path + suffix
+
+
 def _blend_template(t: torch.Tensor, f: torch.Tensor, alpha: float) -> None:
     """SPEC S9 in place on the device: t <- g / |g|, g = (1 - alpha) t + alpha f / |f| (fp32)."""
     g = (1.0 - alpha) * t + alpha * (f / f.norm())
@@ -209,15 +245,7 @@ class Tracker:
     def config_fingerprint(self) -> dict:
         """Every configuration value a tracking frame's arithmetic depends on: a checkpoint records
         these and a resume under any other value is refused instead of drifting from the original run."""
-        c = self.cfg
-        m, p, lk = c["model"], c["particles"], c["likelihood"]
-        return {"arch": self.arch.name, "dtype": str(m["dtype"]), "weights_seed": int(m["weights"]["seed"]),
-                "weights_crc32": self.weights_digest,
-                "mean": [float(v) for v in m["mean"]], "std": [float(v) for v in m["std"]],
-                "P": int(p["num"]), "motion_std": [float(v) for v in p["motion_std"]],
-                "scale_range": [float(v) for v in p["scale_range"]], "seed": int(p["seed"]),
-                "lambda": float(lk["lambda"]), "weight_bits": int(lk["weight_bits"]),
-                "template_update": float(lk["template_update"]), "rank": self.rank, "world_size": self.world_size}
+        return _fingerprint(self.cfg, self.arch.name, self.weights_digest, self.rank, self.world_size)
 
     def state_dict(self) -> dict:
         """The tracker's state between frames as numpy arrays: this rank's particles (after the last resample, so
@@ -235,20 +263,10 @@ class Tracker:
                 "config": np.array(json.dumps(self.config_fingerprint(), sort_keys=True))}
 
     def load_state_dict(self, sd: dict) -> None:
-        import json
-        fmt = int(sd["format"])
-        if fmt == 1:
-            raise ValueError("checkpoint format 1 (rounds 1-2) records only P, rank, world size, seed and arch; format 2 "
-                             "also checks every value the tracking arithmetic depends on (dtype, lambda, motion, "
-                             "weights, ...): re-create the checkpoint with this version")
-        if fmt != 2:
-            raise ValueError(f"unknown checkpoint format {fmt}")
+        _check_fingerprint(sd, self.config_fingerprint())
+        if "n_objects" in sd:
+            raise ValueError("this checkpoint was written by a MultiTracker")
         c = self.cfg
-        saved, mine = json.loads(str(sd["config"])), self.config_fingerprint()
-        diff = sorted(k for k in set(saved) | set(mine) if saved.get(k) != mine.get(k))
-        if diff:
-            raise ValueError("checkpoint was written by a tracker with another configuration or rank layout: "
-                             + ", ".join(f"{k} {saved.get(k)!r} != {mine.get(k)!r}" for k in diff))
         H, W = (int(v) for v in sd["frame_hw"])
         self.box_wh = tuple(float(v) for v in sd["box_wh"])
         t = torch.from_numpy(np.ascontiguousarray(sd["template"], dtype=np.float32)).to(self.device)
@@ -268,10 +286,7 @@ class Tracker:
         self._graph = None
 
     def _checkpoint_file(self, path: str) -> str:
-        """`<path>.rank<r>of<G>.npz` with several ranks, `<path>.npz` with one; a path that already names this
-        rank's file (what save_checkpoint returned) is taken as is, so save -> load round-trips either way."""
-        suffix = f".rank{self.rank}of{self.world_size}.npz" if self.world_size > 1 else ".npz"
-        return path if path.endswith(suffix) else path + suffix
+        return _checkpoint_file(path, self.rank, self.world_size)
 
     def save_checkpoint(self, path: str) -> str:
         """np.savez of state_dict() (no pickled objects); with several ranks each writes `<path>.rank<r>of<G>.npz`.
@@ -327,6 +342,7 @@ class MultiTracker:
             raise ValueError("particles.num must be divisible by the world size")
         self.n_local = self.P // self.world_size
         w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
+        self.weights_digest = weights_digest(w)
         self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, self.K * self.n_local,
                                 c["model"]["mean"], c["model"]["std"])
         self.lam = float(c["likelihood"]["lambda"])
@@ -419,6 +435,59 @@ class MultiTracker:
         f = self.engine.features_many(self._frame_dev, sets, self.boxes)
         for k in range(self.K):
             _blend_template(self.templates[k], f[k], a)
+
+    # ------------------------------------------------------------------ checkpoint / resume (as Tracker)
+    def config_fingerprint(self) -> dict:
+        return {**_fingerprint(self.cfg, self.arch.name, self.weights_digest, self.rank, self.world_size),
+                "n_objects": self.K}
+
+    def state_dict(self) -> dict:
+        """Tracker.state_dict for every target: particles [K][3][P_l], templates [K][D], template boxes [K][2],
+        each filter's frame counter, the frame size and index, and the fingerprint (with the target count)."""
+        import json
+        if not self.pfs:
+            raise RuntimeError("call init(frame, bboxes) first")
+        return {"format": np.int64(2), "n_objects": np.int64(self.K), "frame_index": np.int64(self.frame_index),
+                "pf_frame": np.array([pf.frame for pf in self.pfs], np.int64),
+                "particles": np.stack([pf.particles.cpu().numpy() for pf in self.pfs]),
+                "template": np.stack([t.cpu().numpy() for t in self.templates]),
+                "box_wh": np.array(self.boxes, np.float64),
+                "frame_hw": np.array([self.pfs[0].height, self.pfs[0].width], np.int64),
+                "config": np.array(json.dumps(self.config_fingerprint(), sort_keys=True))}
+
+    def load_state_dict(self, sd: dict) -> None:
+        if "n_objects" not in sd:
+            raise ValueError("this checkpoint was written by a single-target Tracker")
+        _check_fingerprint(sd, self.config_fingerprint())
+        c = self.cfg
+        H, W = (int(v) for v in sd["frame_hw"])
+        boxes = [tuple(float(v) for v in b) for b in sd["box_wh"]]
+        if not self.pfs:
+            self.pfs = [ParticleFilter(self.P, (0.0, 0.0, 1.0), c["particles"]["motion_std"],
+                                       c["particles"]["scale_range"], int(c["particles"]["seed"]) + k, self.device,
+                                       (H, W), self.lam, self.bits, self.rank, self.world_size, self.group)
+                        for k in range(self.K)]
+            self.templates = [torch.empty(self.arch.dim, dtype=torch.float32, device=self.device)
+                              for _ in range(self.K)]
+        self.boxes = boxes
+        for k, pf in enumerate(self.pfs):
+            pf.reset((0.0, 0.0, 1.0))
+            pf.height, pf.width = H, W
+            pf.particles.copy_(torch.from_numpy(np.ascontiguousarray(sd["particles"][k], dtype=np.float32)))
+            pf.frame = int(sd["pf_frame"][k])
+            # in place: a captured graph reads these buffers
+            self.templates[k].copy_(torch.from_numpy(np.ascontiguousarray(sd["template"][k], dtype=np.float32)))
+        self.frame_index = int(sd["frame_index"])
+        self._graph = None
+
+    def save_checkpoint(self, path: str) -> str:
+        path = _checkpoint_file(path, self.rank, self.world_size)
+        np.savez(path, **self.state_dict())
+        return path
+
+    def load_checkpoint(self, path: str) -> None:
+        with np.load(_checkpoint_file(path, self.rank, self.world_size), allow_pickle=False) as z:
+            self.load_state_dict({k: z[k] for k in z.files})
 
     def track(self, frame) -> List[Tuple[float, float, float]]:
         if not self.pfs:
