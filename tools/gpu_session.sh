@@ -86,6 +86,11 @@ for step in "$@"; do
     bench_c4)   # configs[4]'s per-GPU share: 8192 particles, fp8, 1080p
       timeout -k 10 900 python bench.py --preset 4 --particles 8192 --steps 5 --warmup 2 --cpu-baseline off > $OUT/bench_c4.log 2>&1
       ok_or_stop $? bench_c4; tail -1 $OUT/bench_c4.log | cut -c1-400 ;;
+    bench_shares)   # the 2 / 4 / 8-GPU shares of the 4096-particle frame on one GPU (the scaling proxy)
+      for P in 2048 1024 512; do
+        timeout -k 10 600 python bench.py --particles $P --steps 10 --warmup 3 --cpu-baseline off > $OUT/bench_p$P.log 2>&1
+        ok_or_stop $? bench_p$P; tail -1 $OUT/bench_p$P.log | cut -c1-200
+      done ;;
     bench_p512)   # the 8-GPU share of the 4096-particle frame
       timeout -k 10 600 python bench.py --particles 512 --steps 10 --warmup 3 --cpu-baseline off > $OUT/bench_p512.log 2>&1
       ok_or_stop $? bench_p512; tail -1 $OUT/bench_p512.log | cut -c1-400 ;;
