@@ -61,6 +61,11 @@ for step in "$@"; do
       ok_or_stop $? pmc_write
       python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write > $OUT/pmc_traffic.json 2> $OUT/pmc_traffic.err
       ok_or_stop $? pmc_traffic; cat $OUT/pmc_traffic.json | head -40 ;;
+    prof512)   # kernel trace of the 8-GPU share (512 particles): idle gaps between graph kernels
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof512 -o run --output-format csv -- python3 bench.py --particles 512 --steps 5 --warmup 2 --kernel-frames 1 --cpu-baseline off > $OUT/prof512.log 2>&1
+      ok_or_stop $? prof512
+      python tools/trace_gaps.py $OUT/prof512/run_kernel_trace.csv > $OUT/gaps512.txt 2>&1; cat $OUT/gaps512.txt ;;
     pmcmfma)   # MFMA-busy and clock of every kernel of the bench frame (one pass: 2 SQ + 1 GRBM counters)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_mfma -o p --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc_mfma.log 2>&1
