@@ -383,9 +383,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         // issues after the barrier while the MFMA pipes idle. Unconditional, so they stay in this block: past
         // the end they re-read K-tile nk-1 into that K-tile's own slot (identical bytes). Program order B, A
         // keeps the counted vmcnt(4) at the next barrier meaning "B(t+1) has landed".
+        // LAB 14 / 15 / 16 (lab kernels 30 / 31 / 32, round 4, no epilogue): the K loop with the B refills / the A
+        // refills / all refills skipped after the prologue (reads and MFMAs on stale slots, garbage outputs): how much
+        // of the loop the operand DMA bytes cost (a 256 x 384 tile would cut DMA bytes per FLOP by 17 %)
         if constexpr (DEEP && ILV) {
-            stage_b(min(kt + 1, nk - 1));
-            stage_a(min(kt + 2, nk - 1));
+            if constexpr (LAB != 14 && LAB != 16) stage_b(min(kt + 1, nk - 1));
+            if constexpr (LAB != 15 && LAB != 16) stage_a(min(kt + 2, nk - 1));
         }
         if constexpr (MFMAS) {
 #pragma unroll
@@ -447,7 +450,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         }
         return;
     }
-    if constexpr (LAB == 2 || (LAB >= 9 && LAB <= 11)) {
+    if constexpr (LAB == 2 || (LAB >= 9 && LAB <= 11) || (LAB >= 14 && LAB <= 16)) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -1273,6 +1276,17 @@ static int gemm_pf_dist() {   // kernel 27's prefetch distance in K-tiles (VPF_G
         hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 13>), grid, block, 0, s,      \
                            VPF_GEMM_ARGS);                                                                   \
     }                                                                                                        \
+    else if (kern >= 30 && kern <= 32 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {    \
+        if (kern == 30)                                                                                      \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 14>), grid, block, 0, s,  \
+                               VPF_GEMM_ARGS);                                                               \
+        else if (kern == 31)                                                                                 \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 15>), grid, block, 0, s,  \
+                               VPF_GEMM_ARGS);                                                               \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 16>), grid, block, 0, s,  \
+                               VPF_GEMM_ARGS);                                                               \
+    }                                                                                                        \
     else if (kern == 27 && !(VPF_IS_LN(E) && stats_parts > AUX_PARTS) && o8.q == nullptr) {                 \
         hipLaunchKernelGGL((k_gemm_bf16<E, true, false, false, true, true, true, 12>), grid, block, 0, s,      \
                            A, (int)lda, W, bias, residual, pos, patch_rows,                                   \
@@ -1309,7 +1323,7 @@ constexpr bool kGemmLab = false;
 #define VPF_GEMM_LAB_LAUNCH(E)
 #endif
 static bool gemm_kernel_ok(int k) {
-    return (k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9))) || (kGemmLab && k >= 20 && k <= 29);
+    return (k >= 1 && k <= 17 && (kGemmLab || (k != 8 && k != 9))) || (kGemmLab && k >= 20 && k <= 32);
 }
 #define VPF_GEMM_LAUNCH(E)                                                                                   \
     do {                                                                                                     \
