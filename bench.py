@@ -303,8 +303,8 @@ def main() -> int:
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
-    if args.particles % world:
-        raise SystemExit("--particles must be divisible by the number of ranks")
+    if args.particles < world:
+        raise SystemExit("--particles must be at least the number of ranks")
     if args.gpus != world and rank == 0:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 ranks with "
               "python -m torch.distributed.run --nproc-per-node N ... (measuring the ranks that exist)", file=sys.stderr)
@@ -353,7 +353,7 @@ def main() -> int:
     tr.use_graph = use_graph
     tr.engine.timer = None
     ks = timer.summary()
-    n_loc = args.particles // world
+    n_loc = tr.n_local   # rank 0's shard (floor(P / N) particles when N does not divide P)
     M = n_loc * arch.tokens
     D, F = arch.dim, arch.mlp
     flops = {"gemm_fc1": 2.0 * M * D * F, "gemm_fc2": 2.0 * M * F * D, "gemm_qkv": 2.0 * M * D * 3 * D,

@@ -50,15 +50,17 @@ def _read_global(view, P):
 
 def _body(rank, world, P, seed, frames, q):
     rng = np.random.default_rng(seed)
-    n = P // world
-    begin = rank * n
-    chunk = torch.zeros(PF.chunk_words(n), dtype=torch.int32)
+    begin, n = PF.shard_range(P, world, rank)
+    n_max = -(-P // world)
+    even = P % world == 0
+    chunk = torch.zeros(PF.chunk_words(n_max), dtype=torch.int32)
     Ql, local = PF.shard_views(chunk, n)
     local[0], local[1], local[2] = 100.0, 90.0, 1.0
     ref = np.empty((3, P), np.float32)
     ref[0], ref[1], ref[2] = 100.0, 90.0, 1.0
-    allc = torch.zeros(world * PF.chunk_words(n), dtype=torch.int32)
-    view = PF.global_view(allc, world, n)
+    allc = torch.zeros(world * PF.chunk_words(n_max), dtype=torch.int32)
+    cidx = None if even else PF.compact_index(P, world)
+    view = PF.global_view(allc, world, n) if even else None
     results = []
     for k in range(1, frames + 1):
         # identical global weights on every rank; each rank writes only its shard
@@ -73,6 +75,8 @@ def _body(rank, world, P, seed, frames, q):
         pf.predict(ref, 0, 77, k, (3.0, 3.0, 0.05), 224, 224, (0.5, 2.0))
         Ql.copy_(torch.from_numpy(Q[begin:begin + n].copy()))
         PF._all_gather_into(allc, chunk)
+        if not even:   # unequal shards: ParticleFilter._settle's compaction of the gathered chunks
+            view = PF.compact_view(torch.index_select(allc, 0, cidx), P)
         Qg, pg = _read_global(view, P)
         layout_ok = np.array_equal(Qg, Q) and np.array_equal(pg.view(np.uint32), ref.view(np.uint32))
         # device step, emulated: the fixed-order statistics and the global resample, this rank's slots
@@ -90,10 +94,11 @@ def _body(rank, world, P, seed, frames, q):
     q.put((rank, results))
 
 
-@pytest.mark.parametrize("world,P", [(2, 512), (2, 510), (8, 512)])
+@pytest.mark.parametrize("world,P", [(2, 512), (2, 510), (8, 512), (3, 512), (8, 515)])
 def test_two_rank_exchange_matches_oracle(world, P):
-    """world 2 (also with an odd shard: 255 particles, a padded chunk), and world 8 (the driver's 8-GPU layout at
-    4096 particles: 512 per rank; here 64 per rank)."""
+    """world 2 (also with an odd shard: 255 particles, a padded chunk), world 8 (the driver's 8-GPU layout at
+    4096 particles: 512 per rank; here 64 per rank), and unequal shards (512 over 3 ranks: 170 / 171 / 171; 515 over
+    8: 64 or 65 each), whose gathered chunks are compacted into the global order before the device step."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -117,3 +122,28 @@ def test_two_rank_exchange_matches_oracle(world, P):
     for k in range(frames):
         for r in range(1, world):
             assert out[0][k][0] == out[r][k][0]
+
+
+@pytest.mark.parametrize("P,world", [(7, 2), (7, 7), (4096, 8), (4099, 8), (33, 3), (5, 4)])
+def test_shard_range_and_compaction(P, world):
+    """shard_range partitions [0, P) into world contiguous ranges of floor / ceil(P / world) particles in rank order,
+    and compact_index reads the gathered chunks (each laid out by shard_views for its own size inside a slot of the
+    largest chunk) back as the global Q | x | y | s arrays."""
+    ranges = [PF.shard_range(P, world, r) for r in range(world)]
+    assert ranges[0][0] == 0 and sum(n for _, n in ranges) == P
+    assert all(b + n == ranges[r + 1][0] for r, (b, n) in enumerate(ranges[:-1]))
+    assert {n for _, n in ranges} <= {P // world, -(-P // world)}
+    n_max = -(-P // world)
+    cw = PF.chunk_words(n_max)
+    rng = np.random.default_rng(P)
+    Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
+    p = rng.uniform(0, 224, (3, P)).astype(np.float32)
+    allc = torch.full((world * cw,), -1, dtype=torch.int32)   # padding words must never be read
+    for r, (b, n) in enumerate(ranges):
+        Qv, pv = PF.shard_views(allc[r * cw:(r + 1) * cw], n)
+        Qv.copy_(torch.from_numpy(Q[b:b + n].copy()))
+        pv.copy_(torch.from_numpy(p[:, b:b + n].copy()))
+    Qg, pg = _read_global(PF.compact_view(torch.index_select(allc, 0, PF.compact_index(P, world)), P), P)
+    assert np.array_equal(Qg, Q) and np.array_equal(pg, p)
+    with pytest.raises(ValueError):
+        PF.shard_range(3, 4, 0)

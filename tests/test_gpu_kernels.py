@@ -713,9 +713,10 @@ def test_estimate_resample_global(G, P, mode):
     """vpf_estimate_resample (the ParticleFilter product path) over G gathered shard chunks: every rank's slots get
     the global oracle's ancestors and states bit for bit, the resample word drawn on the device equals SPEC S1's,
     T is exact, and the fp64 sums are the same bits for every G (and as vpf_shard_stats over the whole set)."""
-    from vitparticlefiltertracker_amd.particle_filter import chunk_words, global_view, shard_views
-    if P % G:
-        pytest.skip("P not divisible by G")
+    from vitparticlefiltertracker_amd.particle_filter import (chunk_words, compact_index, compact_view, global_view,
+                                                                shard_range, shard_views)
+    if G > P:
+        pytest.skip("more ranks than particles")
     rng = np.random.default_rng(P + G)
     Q = rng.integers(0, 1 << 40, P, dtype=np.int64)
     if mode == "sparse":
@@ -729,15 +730,17 @@ def test_estimate_resample_global(G, P, mode):
     seed, frame = (1 << 40) + 17 * P, 9
     ref = pf.resample(Q, pf.resample_U(seed, frame))
     T_ref, sums_ref = pf.shard_stats(Q, p)
-    n = P // G
-    cw = chunk_words(n)
+    n_max = -(-P // G)   # unequal shards (P = 7 over 2): chunks sized for the largest, compacted as ParticleFilter does
+    cw = chunk_words(n_max)
     allc = torch.zeros(G * cw, dtype=torch.int32)
     for r in range(G):
+        b, n = shard_range(P, G, r)
         Qv, pv = shard_views(allc[r * cw:(r + 1) * cw], n)
-        Qv.copy_(torch.from_numpy(Q[r * n:(r + 1) * n].copy()))
-        pv.copy_(torch.from_numpy(p[:, r * n:(r + 1) * n].copy()))
+        Qv.copy_(torch.from_numpy(Q[b:b + n].copy()))
+        pv.copy_(torch.from_numpy(p[:, b:b + n].copy()))
     allc = allc.to(DEV)
-    view = global_view(allc, G, n)
+    view = (global_view(allc, G, n_max) if P % G == 0
+            else compact_view(torch.index_select(allc, 0, compact_index(P, G).to(DEV)), P))
     # the world-1 form ParticleFilter passes: its own Q and particle arrays, one shard of P
     Qd, pd = torch.from_numpy(Q).to(DEV), torch.from_numpy(p).to(DEV)
     view1 = (Qd, P, pd.view(-1), P, 3 * P, P)
@@ -759,12 +762,13 @@ def test_estimate_resample_global(G, P, mode):
     else:   # uniform fallback: the plain sums (estimate = sum / P)
         np.testing.assert_allclose(s1[1:].view(torch.float64).numpy(), p.astype(np.float64).sum(axis=1), rtol=1e-13)
     for r in range(G):
+        b, n = shard_range(P, G, r)
         anc = torch.full((n,), -1, device=DEV, dtype=torch.int32)
         st = torch.empty(3, n, device=DEV)
         stats = torch.empty(4, device=DEV, dtype=torch.int64)
-        vpf().estimate_resample(*view, P, seed, frame, r * n, (r + 1) * n, anc, st, cdf, stats)
-        assert np.array_equal(anc.cpu().numpy(), ref[r * n:(r + 1) * n]), f"shard {r}: ancestors"
-        assert np.array_equal(st.cpu().numpy().view(np.uint32), p[:, ref[r * n:(r + 1) * n]].view(np.uint32))
+        vpf().estimate_resample(*view, P, seed, frame, b, b + n, anc, st, cdf, stats)
+        assert np.array_equal(anc.cpu().numpy(), ref[b:b + n]), f"shard {r}: ancestors"
+        assert np.array_equal(st.cpu().numpy().view(np.uint32), p[:, ref[b:b + n]].view(np.uint32))
         assert torch.equal(stats.cpu(), s1), f"shard {r}: statistics bits depend on G"
 
 

@@ -56,9 +56,12 @@ def _worker(rank, world, port, P, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,P", [(2, 256), (4, 256), (3, 33)])
+@pytest.mark.parametrize("world,P", [(2, 256), (4, 256), (3, 33), (3, 100)])
 def test_sharded_tracker_equals_single_rank(world, P):
-    """(3, 33): 11 particles per rank, an odd (padded) shard chunk and a world size that is not a power of two."""
+    """(3, 33): 11 particles per rank, an odd (padded) shard chunk and a world size that is not a power of two.
+    (3, 100): unequal shards (33 / 33 / 34; SURVEY.md §8e's [floor(rP/G), floor((r+1)P/G)) ranges), compacted into the
+    global order after the gather."""
+    from vitparticlefiltertracker_amd.particle_filter import shard_range
     from vitparticlefiltertracker_amd import Tracker
     from vitparticlefiltertracker_amd.frames import synthetic_clip
     ref = _run(Tracker(_cfg(P), device="cuda:0"), synthetic_clip(FRAMES + 1))
@@ -72,14 +75,14 @@ def test_sharded_tracker_equals_single_rank(world, P):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    n = P // world
     for r in range(world):
         assert not isinstance(out[r], str), out[r]
+        b, n = shard_range(P, world, r)
         for k, ((est, anc, parts), (est1, anc1, parts1)) in enumerate(zip(out[r], ref), start=1):
             # every rank sums the gathered global set in one fixed order: the single-rank estimate's bits
             assert est == est1, f"rank {r} frame {k}: estimate {est} vs single rank {est1}"
-            assert np.array_equal(anc, anc1[r * n:(r + 1) * n]), f"rank {r} frame {k}: ancestors"
-            assert np.array_equal(parts.view(np.uint32), parts1[:, r * n:(r + 1) * n].view(np.uint32)), \
+            assert np.array_equal(anc, anc1[b:b + n]), f"rank {r} frame {k}: ancestors"
+            assert np.array_equal(parts.view(np.uint32), parts1[:, b:b + n].view(np.uint32)), \
                 f"rank {r} frame {k}: particle states"
     for k in range(FRAMES):
         assert all(out[r][k][0] == out[0][k][0] for r in range(world)), f"frame {k + 1}: ranks disagree"
@@ -146,15 +149,17 @@ def _mt_sharded(world, P, dtype="bf16", alpha=0.0):
     return out
 
 
-@pytest.mark.parametrize("world,P,alpha", [(2, 128, 0.0), (3, 33, 0.5)])
+@pytest.mark.parametrize("world,P,alpha", [(2, 128, 0.0), (3, 33, 0.5), (2, 45, 0.5)])
 def test_sharded_multitracker_equals_single_rank_and_oracle(world, P, alpha):
     """Two targets with different boxes, each target's particles sharded over the ranks (bf16):
     * every rank returns the single-rank MultiTracker's estimates bit for bit, and its shards of every target's
       weights, ancestors and states;
     * against the oracle directly: the ranks' weight shards, concatenated in rank order, injected into
       OracleMultiTracker give every rank's ancestors and states bit for bit and the estimates to 1e-12, every frame.
-    (3, 33): 11 particles per rank per target, odd shard chunks; alpha = 0.5: the template update on every rank."""
+    (3, 33): 11 particles per rank per target, odd shard chunks; alpha = 0.5: the template update on every rank.
+    (2, 45): unequal shards (22 / 23 per target)."""
     from oracle.tracker import OracleMultiTracker
+    from vitparticlefiltertracker_amd.particle_filter import shard_range
     from vitparticlefiltertracker_amd import MultiTracker
     from vitparticlefiltertracker_amd.config import ARCHS
     from vitparticlefiltertracker_amd.frames import synthetic_clip
@@ -163,15 +168,15 @@ def test_sharded_multitracker_equals_single_rank_and_oracle(world, P, alpha):
     clip = synthetic_clip(FRAMES + 1)
     ref = _mt_run(MultiTracker(cfg, n_objects=len(BOXES), device="cuda:0"), clip)
     out = _mt_sharded(world, P, "bf16", alpha)
-    n = P // world
     K = len(BOXES)
+    sl = [slice(b, b + n) for b, n in (shard_range(P, world, r) for r in range(world))]
     for r in range(world):
         for k, ((ests, ancs, parts, Qs), (ests1, ancs1, parts1, Qs1)) in enumerate(zip(out[r], ref), start=1):
             assert ests == ests1, f"rank {r} frame {k}: estimates {ests} vs single rank {ests1}"
             for t in range(K):
-                assert np.array_equal(Qs[t], Qs1[t][r * n:(r + 1) * n]), f"rank {r} frame {k} target {t}: weights"
-                assert np.array_equal(ancs[t], ancs1[t][r * n:(r + 1) * n]), f"rank {r} frame {k} target {t}"
-                assert np.array_equal(parts[t].view(np.uint32), parts1[t][:, r * n:(r + 1) * n].view(np.uint32))
+                assert np.array_equal(Qs[t], Qs1[t][sl[r]]), f"rank {r} frame {k} target {t}: weights"
+                assert np.array_equal(ancs[t], ancs1[t][sl[r]]), f"rank {r} frame {k} target {t}"
+                assert np.array_equal(parts[t].view(np.uint32), parts1[t][:, sl[r]].view(np.uint32))
     arch = ARCHS["vit_tiny_patch16_224"]
     om = OracleMultiTracker(cfg, K, make_vit_weights(arch, seed=3), arch)
     om.init(clip[0], BOXES)
@@ -181,9 +186,9 @@ def test_sharded_multitracker_equals_single_rank_and_oracle(world, P, alpha):
         for r in range(world):
             for t in range(K):
                 np.testing.assert_allclose(out[r][k][0][t], e_ref[t], rtol=1e-12)
-                assert np.array_equal(out[r][k][1][t], om.targets[t].last_ancestors[r * n:(r + 1) * n]), (r, k, t)
+                assert np.array_equal(out[r][k][1][t], om.targets[t].last_ancestors[sl[r]]), (r, k, t)
                 assert np.array_equal(out[r][k][2][t].view(np.uint32),
-                                      om.targets[t].particles[:, r * n:(r + 1) * n].view(np.uint32)), (r, k, t)
+                                      om.targets[t].particles[:, sl[r]].view(np.uint32)), (r, k, t)
 
 
 def test_sharded_multitracker_fp32_matches_oracle():

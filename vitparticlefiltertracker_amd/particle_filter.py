@@ -1,10 +1,12 @@
 """`ParticleFilter` — the reference's "Particle Filter ... probabilistic algorithms for accurate state
 estimation" (/root/reference/README.md:8), SPEC.md S2/S5-S7, on the HIP path.
 
-Particles are sharded by index across ranks (rank r owns [r*P/G, (r+1)*P/G)); one process per GPU.
+Particles are sharded by index across ranks (rank r owns [floor(r*P/G), floor((r+1)*P/G)); shards
+differ by at most one particle when G does not divide P); one process per GPU.
 Per frame the only cross-device traffic is ONE fixed-size all-gather of the shard chunks (weight Q_i int64 +
-state x, y, s fp32 = 20 B per particle; 80 KB at 4096 particles, 1.3 MB at configs[4]'s 65536). Every rank then
-holds the global weights and states, and one device call (vpf_estimate_resample) computes on each rank:
+state x, y, s fp32 = 20 B per particle; 80 KB at 4096 particles, 1.3 MB at configs[4]'s 65536; every chunk is sized
+for the largest shard). Every rank then holds the global weights and states, and one device call
+(vpf_estimate_resample) computes on each rank:
 
   * the weight-normalisation sum T and the estimate sums (SPEC S6), in one fixed-order tree over the GLOBAL
     index, so every rank and every world size gets the same bits;
@@ -68,15 +70,26 @@ def slot_range(offset: int, shard_T: int, T: int, P: int, U: int) -> Tuple[int, 
     return first_at_least(offset), first_at_least(offset + shard_T)
 
 
-def plan_resample(stats, P: int, n_local: int, U: int):
+def shard_range(P: int, world: int, rank: int) -> Tuple[int, int]:
+    """(begin, n) of rank `rank`'s particles: [floor(rank P / world), floor((rank + 1) P / world)).
+    Equal shards when world divides P; otherwise the sizes differ by one. Needs 1 <= world <= P."""
+    if not 1 <= world <= P or not 0 <= rank < world:
+        raise ValueError(f"need 1 <= world_size <= particles and 0 <= rank < world_size (P={P}, world={world}, "
+                         f"rank={rank})")
+    b, e = rank * P // world, (rank + 1) * P // world
+    return b, e - b
+
+
+def plan_resample(stats, P: int, n_local, U: int):
     """Host plan of the exact systematic resample (SPEC S7) for the per-shard entry point vpf_resample, from the
-    shards' (T_r, ...) statistics: (uniform, T, offsets, slot ranges per rank). ParticleFilter itself runs the
-    device-resident vpf_estimate_resample and needs no plan."""
+    shards' (T_r, ...) statistics: (uniform, T, offsets, slot ranges per rank). `n_local`: the shard size (equal
+    shards) or the list of shard sizes. ParticleFilter itself runs the device-resident vpf_estimate_resample and
+    needs no plan."""
     world = len(stats)
     T_r = [s[0] for s in stats]
     uniform = sum(T_r) == 0
     if uniform:
-        T_r = [n_local] * world
+        T_r = list(n_local) if isinstance(n_local, (list, tuple)) else [n_local] * world
     T = sum(T_r)
     offsets = [sum(T_r[:r]) for r in range(world)]
     ranges = [slot_range(offsets[r], T_r[r], T, P, U) for r in range(world)]
@@ -113,6 +126,27 @@ def global_view(allc: torch.Tensor, world: int, n: int):
     return allc.view(torch.int64), cw // 2, allc[2 * n:].view(torch.float32), n, cw, n
 
 
+def compact_index(P: int, world: int) -> torch.Tensor:
+    """Unequal shards (world does not divide P): int32-word indices into the gathered chunks (world slots of
+    chunk_words(ceil(P / world)) words; rank r's slot holds its shard_views layout for its own n_r) that read out
+    the global arrays in particle order: Q int64[P] as 2P words, then x | y | s fp32[P]. One index_select of the
+    gathered buffer with it gives the one-shard layout that vpf_estimate_resample reads as (Q, P, x|y|s, P, 3P, P)."""
+    cw = chunk_words(-(-P // world))
+    q, st = [], [[], [], []]
+    for r in range(world):
+        _, n = shard_range(P, world, r)
+        base = r * cw
+        q.append(torch.arange(base, base + 2 * n))
+        for c in range(3):
+            st[c].append(torch.arange(base + (2 + c) * n, base + (3 + c) * n))
+    return torch.cat(q + st[0] + st[1] + st[2])
+
+
+def compact_view(glob: torch.Tensor, P: int):
+    """vpf_estimate_resample's arguments over the compacted global arrays (glob: int32[5P], compact_index order)."""
+    return glob[: 2 * P].view(torch.int64), P, glob[2 * P:].view(torch.float32), P, 3 * P, P
+
+
 class ParticleFilter:
     """H1, H10-H12. API: predict(), update(features, template), estimate(), resample(),
     attributes `particles` (float32[3][P_local] on the device, SoA rows x, y, scale) and `Q` (int64[P_local]).
@@ -127,27 +161,32 @@ class ParticleFilter:
                  scale_range=(0.5, 2.0), seed: int = 1234, device=None, frame_size=(224, 224),
                  lam: float = 20.0, weight_bits: int = 40, rank: int = 0, world_size: int = 1,
                  group: Optional[object] = None):
-        if world_size < 1 or num_particles % world_size:
-            raise ValueError("num_particles must be divisible by world_size")
+        self.begin, self.n_local = shard_range(int(num_particles), int(world_size), int(rank))
         if weight_bits + max(1, (num_particles - 1).bit_length()) > 62:
             raise ValueError("weight_bits + ceil(log2 P) must be <= 62 (SPEC S5)")
         if not (math.isfinite(float(lam)) and float(lam) >= 0.0):
             raise ValueError("lam must be finite and >= 0 (SPEC S5)")
         self.P = int(num_particles)
         self.rank, self.world_size, self.group = int(rank), int(world_size), group
-        self.n_local = n = self.P // self.world_size
-        self.begin = self.rank * self.n_local
+        n = self.n_local
+        n_max = -(-self.P // self.world_size)     # every rank's chunk has the largest shard's size (fixed-size gather)
         self.motion_std = [float(v) for v in motion_std]
         self.scale_range = [float(v) for v in scale_range]
         self.seed = int(seed)
         self.lam, self.bits = float(lam), int(weight_bits)
         self.height, self.width = int(frame_size[0]), int(frame_size[1])
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self._chunk = torch.zeros(chunk_words(n), device=self.device, dtype=torch.int32)
+        self._chunk = torch.zeros(chunk_words(n_max), device=self.device, dtype=torch.int32)
         self.Q, self.particles = shard_views(self._chunk, n)
+        self._cidx = None
         if self.world_size > 1:
-            self._allc = torch.zeros(self.world_size * chunk_words(n), device=self.device, dtype=torch.int32)
-            self._gview = global_view(self._allc, self.world_size, n)
+            self._allc = torch.zeros(self.world_size * chunk_words(n_max), device=self.device, dtype=torch.int32)
+            if self.P % self.world_size == 0:
+                self._gview = global_view(self._allc, self.world_size, n)
+            else:   # unequal shards: the gathered chunks are compacted into the global order first (_settle)
+                self._cidx = compact_index(self.P, self.world_size).to(self.device)
+                self._glob = torch.empty(5 * self.P, device=self.device, dtype=torch.int32)
+                self._gview = compact_view(self._glob, self.P)
         else:
             self._gview = (self.Q, n, self.particles.view(-1), n, 3 * n, n)
         self._cdf = torch.empty(self.P, device=self.device, dtype=torch.int64)
@@ -202,6 +241,8 @@ class ParticleFilter:
             return
         if self.world_size > 1:
             _all_gather_into(self._allc, self._chunk, self.group)
+            if self._cidx is not None:
+                torch.index_select(self._allc, 0, self._cidx, out=self._glob)
         Qv, qs, Pv, ld, ps, nsh = self._gview
         vpf.estimate_resample(Qv, qs, Pv, ld, ps, nsh, self.P, self.seed, self.frame, self.begin,
                               self.begin + self.n_local, self._anc, self._states, self._cdf, self._stats_dev)

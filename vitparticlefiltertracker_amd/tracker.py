@@ -21,7 +21,7 @@ import torch
 
 from . import _lib
 from .config import arch_of, load_config
-from .particle_filter import ParticleFilter
+from .particle_filter import ParticleFilter, shard_range
 from .vit import ViTEngine
 from .weights import make_vit_weights
 
@@ -105,9 +105,7 @@ class Tracker:
         c = self.cfg
         self.arch = arch_of(c)
         P = int(c["particles"]["num"])
-        if P % self.world_size:
-            raise ValueError("particles.num must be divisible by the world size")
-        self.n_local = P // self.world_size
+        _, self.n_local = shard_range(P, self.world_size, self.rank)   # rank r: [floor(rP/G), floor((r+1)P/G))
         w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
         self.weights_digest = weights_digest(w)
         self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, max(1, self.n_local),
@@ -338,9 +336,7 @@ class MultiTracker:
         self.arch = arch_of(c)
         self.K = int(n_objects)
         self.P = int(c["particles"]["num"])
-        if self.P % self.world_size:
-            raise ValueError("particles.num must be divisible by the world size")
-        self.n_local = self.P // self.world_size
+        _, self.n_local = shard_range(self.P, self.world_size, self.rank)
         w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
         self.weights_digest = weights_digest(w)
         self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, self.K * self.n_local,
