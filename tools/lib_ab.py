@@ -3,7 +3,7 @@ libvpf.so (bound by vitparticlefiltertracker_amd._lib) and another build loaded 
 the lab build, tools/gemm_lab -> libvpf_lab.so, whose MX8 GEMM / attention are the round-3 snapshots). Both get the
 same device buffers; interleaved rounds, HIP-event medians, outputs compared bit for bit.
 
-Cases: mx8_fc1 (LN + GELU, MX8-only output: FC2's A operand), mx8_fc2 (residual + planes + the MX8 copy of h),
+Cases: bf16_qkv / bf16_proj / bf16_fc1 / bf16_fc2 (vpf_gemm_bf16 with the encoder's epilogues), mx8_fc1 (LN + GELU, MX8-only output: FC2's A operand), mx8_fc2 (residual + planes + the MX8 copy of h),
 mx8_qkv (LN fold, bf16 out), quant (vpf_quantize_mx8 of a bf16 [M][768] tensor), attn (bf16 attention, N = 197),
 attn577 (bf16 attention at ViT-L/14 @ 336's N = 577, 16 heads).
 
@@ -33,6 +33,7 @@ def main():
         L.vpf_gemm_mx8.argtypes = E.SIGNATURES["vpf_gemm_mx8"]
         L.vpf_quantize_mx8.argtypes = E.SIGNATURES["vpf_quantize_mx8"]
         L.vpf_attention_bf16.argtypes = E.SIGNATURES["vpf_attention_bf16"]
+        L.vpf_gemm_bf16.argtypes = E.SIGNATURES["vpf_gemm_bf16"]
     M = int(os.environ.get("AB_M", 4096 * 197))
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -59,6 +60,34 @@ def main():
                 q, s = bufs[k]
                 return L.vpf_quantize_mx8(pt(x), 768, M, 768, 1, pt(q), q.stride(0), pt(s), s.shape[1], st)
             flop = 0.0
+        elif case.startswith("bf16_"):
+            # the bf16 GEMMs with their product epilogues: qkv (LN fold), proj / fc2 (residual in place + statistics
+            # planes), fc1 (LN fold + GELU); LN statistics planes of the A operand itself
+            N, K, epi = {"bf16_qkv": (2304, 768, E.VPF_EPI_LN), "bf16_proj": (768, 768, E.VPF_EPI_BIAS_RESIDUAL),
+                         "bf16_fc1": (3072, 768, E.VPF_EPI_LN_GELU),
+                         "bf16_fc2": (768, 3072, E.VPF_EPI_BIAS_RESIDUAL)}[case]
+            a = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+            w = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16)
+            bias = torch.rand(N, device=dev, generator=g) * 0.1
+            colsum = w.float().sum(1).contiguous()
+            af = a.float().view(M, K // 64, 64)
+            planes = torch.stack([af.sum(2), (af * af).sum(2)], 2).transpose(0, 1).contiguous()   # [K/64][M][2]
+            res0 = (torch.rand(M, N, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+            resid = epi == E.VPF_EPI_BIAS_RESIDUAL
+            bufs = {}
+            for k in ("product", "other"):
+                out = res0.clone() if resid else torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+                bufs[k] = (out, torch.empty(N // 64, M, 2, device=dev) if resid else None)
+
+            def call(L, k, reset=False):
+                out, so = bufs[k]
+                if resid and reset:
+                    out.copy_(res0)
+                return L.vpf_gemm_bf16(pt(a), K, pt(w), pt(bias), pt(out) if resid else None, None, 0,
+                                       None if resid else pt(planes), None if resid else pt(colsum), pt(out), N, M, N, K,
+                                       epi, 0 if resid else K // 64, 1e-6, pt(so) if resid else None, None, 0, None, 0,
+                                       st)
+            flop = 2.0 * M * N * K
         else:
             N, K = {"mx8_fc1": (3072, 768), "mx8_fc2": (768, 3072), "mx8_qkv": (2304, 768)}[case]
             a = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
@@ -91,13 +120,13 @@ def main():
                                       0 if fc2 else Pn, 1e-6, pt(pl) if fc2 else None, st)
             flop = 2.0 * M * N * K
         for k, L in (("product", P), ("other", O)):
-            assert (call(L, k, reset=True) if case.startswith("mx8") else call(L, k)) == 0, (case, k)
+            assert (call(L, k, reset=True) if case.startswith(("mx8", "bf16")) else call(L, k)) == 0, (case, k)
         torch.cuda.synchronize()
         def snap(k):   # the outputs the call writes
             b = bufs[k]
             if case == "mx8_fc1":
                 b = b[1:3]
-            elif case == "mx8_qkv":
+            elif case == "mx8_qkv" or case in ("bf16_qkv", "bf16_fc1"):
                 b = b[:1]
             return [t.clone() for t in (b if isinstance(b, (tuple, list)) else (b,)) if t is not None]
         same = all(torch.equal(x, y) for x, y in zip(snap("product"), snap("other")))
