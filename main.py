@@ -23,7 +23,9 @@ def main(argv=None) -> int:
     ap.add_argument("--frames", type=int, default=None, help="override input.frames")
     ap.add_argument("--out", default=None, help="write positions as JSON here")
     ap.add_argument("--video-out", default=None,
-                    help="write the frames with the tracked box drawn: a .y4m file, or a directory of .ppm frames")
+                    help="write the frames with the tracked box drawn: a .y4m file, or a directory of frames")
+    ap.add_argument("--frame-format", default="ppm", choices=["ppm", "png", "jpg"],
+                    help="image format of the --video-out directory's frames (png / jpg through Pillow)")
     ap.add_argument("--checkpoint", default=None,
                     help="save the tracker state (np.savez; per rank with several GPUs) here after the last frame")
     ap.add_argument("--checkpoint-every", type=int, default=0, help="also save every N frames")
@@ -34,8 +36,7 @@ def main(argv=None) -> int:
     import torch
     import torch.distributed as dist
     from vitparticlefiltertracker_amd import MultiTracker, Tracker, load_config
-    from vitparticlefiltertracker_amd.frames import (Y4MWriter, draw_box, iter_frames, prefetch, synthetic_clip,
-                                                      write_ppm)
+    from vitparticlefiltertracker_amd.frames import Y4MWriter, draw_box, iter_frames, prefetch, synthetic_clip
 
     cfg = load_config(args.config)
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
@@ -78,7 +79,7 @@ def main(argv=None) -> int:
         if sink is not None:
             sink.write(img)
         else:
-            write_ppm(os.path.join(args.video_out, f"frame_{k:05d}.ppm"), img)
+            _write_frame(args, k, img)
 
     if not args.resume:
         emit(0, first, inp["bbox0"])
@@ -108,8 +109,8 @@ def main(argv=None) -> int:
 
 
 def _sink(args, rank):
-    """(emit(k, rgb, boxes), close()) for --video-out: the frame with every box drawn, as .y4m or PPM frames."""
-    from vitparticlefiltertracker_amd.frames import Y4MWriter, draw_box, write_ppm
+    """(emit(k, rgb, boxes), close()) for --video-out: the frame with every box drawn, as .y4m or image frames."""
+    from vitparticlefiltertracker_amd.frames import Y4MWriter, draw_box
     if not args.video_out or rank != 0:
         return (lambda k, rgb, boxes: None), (lambda: None)
     writer = Y4MWriter(args.video_out) if args.video_out.lower().endswith(".y4m") else None
@@ -123,8 +124,18 @@ def _sink(args, rank):
         if writer is not None:
             writer.write(img)
         else:
-            write_ppm(os.path.join(args.video_out, f"frame_{k:05d}.ppm"), img)
+            _write_frame(args, k, img)
     return emit, (writer.close if writer is not None else (lambda: None))
+
+
+def _write_frame(args, k, img) -> None:
+    """Frame k of a --video-out directory in --frame-format (PPM with numpy; PNG / JPEG through Pillow)."""
+    from vitparticlefiltertracker_amd.frames import write_image_pil, write_ppm
+    path = os.path.join(args.video_out, f"frame_{k:05d}.{args.frame_format}")
+    if args.frame_format == "ppm":
+        write_ppm(path, img)
+    else:
+        write_image_pil(path, img)
 
 
 def _run_multi(args, cfg, boxes, frames, MultiTracker, dist) -> int:

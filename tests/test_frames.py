@@ -142,3 +142,28 @@ def test_y4m_writer_streams(tmp_path):
         with fr.Y4MWriter(tmp_path / "x.y4m") as w:
             w.write(clip[0])
             w.write(clip[0][:5])
+
+
+def test_pillow_images_and_directory(tmp_path):
+    """PNG (lossless: exact), JPEG (lossy: close), BMP and a grey PNG through Pillow, alone and mixed with PPM / .npy
+    frames in one directory (sorted by name); and the writer main.py's --frame-format uses."""
+    clip = _clip(5)
+    d = tmp_path / "mixed"
+    d.mkdir()
+    fr.write_image_pil(d / "f000.png", clip[0])
+    fr.write_ppm(d / "f001.ppm", clip[1])
+    yy, xx = np.mgrid[: clip.shape[1], : clip.shape[2]]
+    smooth = np.stack([xx * 9, yy * 13, (xx + yy) * 5], 2).astype(np.uint8)   # JPEG is meant for smooth images
+    fr.write_image_pil(d / "f002.jpg", smooth, quality=98)
+    fr.write_image_pil(d / "f003.bmp", clip[3])
+    grey = clip[4, ..., 0]
+    from PIL import Image
+    Image.fromarray(grey, "L").save(d / "f004.png")
+    out = list(fr.iter_frames(str(d)))
+    assert len(out) == 5 and all(o.dtype == np.uint8 and o.shape == clip[0].shape for o in out)
+    np.testing.assert_array_equal(out[0], clip[0])
+    np.testing.assert_array_equal(out[1], clip[1])
+    assert np.abs(out[2].astype(int) - smooth.astype(int)).mean() < 3     # lossy
+    np.testing.assert_array_equal(out[3], clip[3])
+    np.testing.assert_array_equal(out[4], np.repeat(grey[..., None], 3, 2))
+    np.testing.assert_array_equal(next(fr.iter_frames(str(d / "f000.png"))), clip[0])

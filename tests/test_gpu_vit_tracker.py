@@ -243,6 +243,38 @@ def test_main_video_out(tmp_path):
     assert red.sum() > 100                          # the box outline is there
 
 
+def test_main_png_frames_in_and_out(tmp_path):
+    """main.py on a directory of PNG frames (read through Pillow), writing PNG frames with --frame-format png: the
+    positions equal those of the same clip given as a .npy file (PNG is lossless), and every output frame exists."""
+    import json
+    import sys
+    import yaml
+    from vitparticlefiltertracker_amd.frames import read_image_pil, synthetic_clip, write_image_pil
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+    import main as vpf_main
+    clip = synthetic_clip(4)
+    src = tmp_path / "png_in"
+    src.mkdir()
+    for k, f in enumerate(clip):
+        write_image_pil(src / f"{k:03d}.png", f)
+    np.save(tmp_path / "clip.npy", clip)
+    outs = []
+    for name, source in (("png", src), ("npy", tmp_path / "clip.npy")):
+        cfg = {"model": {"arch": "vit_tiny_patch16_224", "dtype": "bf16"}, "particles": {"num": 64, "seed": 3},
+               "input": {"source": str(source), "frames": 4}}
+        cpath = tmp_path / f"{name}.yaml"
+        cpath.write_text(yaml.safe_dump(cfg))
+        o = tmp_path / f"{name}.json"
+        argv = ["--config", str(cpath), "--out", str(o)]
+        if name == "png":
+            argv += ["--video-out", str(tmp_path / "png_out"), "--frame-format", "png"]
+        assert vpf_main.main(argv) == 0
+        outs.append(json.loads(o.read_text()))
+    assert outs[0] == outs[1] and len(outs[0]) == 3
+    written = sorted((tmp_path / "png_out").glob("frame_*.png"))
+    assert len(written) == 4 and read_image_pil(written[0]).shape == (224, 224, 3)
+
+
 def test_main_multi_object(tmp_path):
     """main.py with input.bboxes (README.md:46-50, SPEC S9): one MultiTracker over two targets; the JSON has one record
     per frame with both targets, target 0's track is main.py's single-target track bit for bit (the batched pass is

@@ -1,7 +1,8 @@
 """Frame sources — the metric's synthetic clip, plus plain readers for the "video
-feed or images" the reference reads (README.md:42) but never ships. No cv2 / torchvision / PIL in this image, so
-the readers are numpy: `.npy` clips, raw YUV4MPEG2 video (`.y4m`, what `ffmpeg -f yuv4mpegpipe` writes),
-binary PPM/PGM images, and directories of `.npy` / `.ppm` / `.pgm` frames.
+feed or images" the reference reads (README.md:42) but never ships. No cv2 / torchvision in this image, so the
+readers are numpy: `.npy` clips, raw YUV4MPEG2 video (`.y4m`, what `ffmpeg -f yuv4mpegpipe` writes), binary PPM/PGM
+images, and directories of frames. Compressed images (PNG, JPEG, BMP, TIFF, WebP) go through Pillow when it is
+importable (it is in this image; imported on first use, with a clear error otherwise).
 
 `prefetch(frames, depth)` decodes ahead on a host thread into pinned buffers, so a clip's decode (numpy YUV->RGB
 of a 1080p frame is tens of ms) overlaps the previous frame's GPU work; `Tracker.track` takes the pinned tensor
@@ -248,19 +249,51 @@ def write_ppm(path, rgb: np.ndarray) -> None:
         fh.write(np.ascontiguousarray(rgb, dtype=np.uint8).tobytes())
 
 
+# ---------------------------------------------------------------------------------------------- Pillow formats
+_PIL_EXT = (".png", ".jpg", ".jpeg", ".bmp", ".tif", ".tiff", ".webp")
+
+
+def _pil():
+    try:
+        from PIL import Image
+    except ImportError as e:   # pragma: no cover - Pillow is in this image
+        raise RuntimeError("reading or writing PNG / JPEG / BMP / TIFF / WebP frames needs Pillow (PIL), which is not "
+                           "importable here; convert the frames to .ppm / .npy / .y4m") from e
+    return Image
+
+
+def read_image_pil(path) -> np.ndarray:
+    """uint8[H][W][3] RGB of one PNG / JPEG / BMP / TIFF / WebP image (grey, palette and alpha images converted to
+    RGB; the first frame of a multi-frame file)."""
+    with _pil().open(path) as im:
+        return np.ascontiguousarray(np.asarray(im.convert("RGB"), dtype=np.uint8))
+
+
+def write_image_pil(path, rgb: np.ndarray, quality: int = 95) -> None:
+    """Write uint8[H][W][3] RGB in the format the file suffix names (PNG lossless; JPEG at `quality`)."""
+    im = _pil().fromarray(np.ascontiguousarray(rgb, dtype=np.uint8), "RGB")
+    if os.fspath(path).lower().endswith((".jpg", ".jpeg")):
+        im.save(path, quality=int(quality))
+    else:
+        im.save(path)
+
+
 # ---------------------------------------------------------------------------------------------- dispatch
-_IMAGE_EXT = (".npy", ".ppm", ".pgm", ".pnm")
+_IMAGE_EXT = (".npy", ".ppm", ".pgm", ".pnm") + _PIL_EXT
 
 
 def _read_image(p) -> np.ndarray:
-    if p.lower().endswith(".npy"):
+    low = p.lower()
+    if low.endswith(".npy"):
         return np.load(p, allow_pickle=False)
+    if low.endswith(_PIL_EXT):
+        return read_image_pil(p)
     return read_pnm(p)
 
 
 def iter_frames(source) -> Iterator[np.ndarray]:
-    """Yield uint8[H][W][3] frames from a clip array, a `.npy` clip, a `.y4m` video, a single PPM/PGM image, or a
-    directory of `.npy` / `.ppm` / `.pgm` frames (sorted by name)."""
+    """Yield uint8[H][W][3] frames from a clip array, a `.npy` clip, a `.y4m` video, a single image (PPM/PGM, or
+    PNG / JPEG / BMP / TIFF / WebP through Pillow), or a directory of such frames (sorted by name)."""
     if isinstance(source, np.ndarray):
         arr = source if source.ndim == 4 else source[None]
         for f in arr:
@@ -278,6 +311,9 @@ def iter_frames(source) -> Iterator[np.ndarray]:
         return
     if low.endswith((".ppm", ".pgm", ".pnm")):
         yield read_pnm(path)
+        return
+    if low.endswith(_PIL_EXT):
+        yield read_image_pil(path)
         return
     arr = np.load(path, mmap_mode="r", allow_pickle=False)
     for f in (arr if arr.ndim == 4 else arr[None]):
