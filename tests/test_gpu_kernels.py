@@ -822,3 +822,40 @@ def test_gemm_splitk_rejects_bad_split():
     with pytest.raises(Exception):   # 768 is not a multiple of 64 * 5
         vpf().gemm_splitk_(A, W, torch.zeros(768, device=DEV), None, None, None, 0, 5, out, None,
                            torch.empty(5 * 4 * 768, device=DEV))
+
+
+def test_particle_filter_api_matches_oracle():
+    """The ParticleFilter surface driven directly, 1000 particles over 5 frames: predict() equals the
+    oracle's S2 walk bit for bit; update(features, template) gives Q = weights_to_Q of the kernel's cosine (itself
+    within 1e-5 of numpy's); estimate() equals the oracle's S6 estimate; resample() returns the oracle's S7
+    ancestors and the particles become their states; `states` is the [P][3] view of the same storage."""
+    from vitparticlefiltertracker_amd.particle_filter import ParticleFilter
+    P, D, seed = 1000, 192, 321
+    std, srange = (3.0, 2.0, 0.03), (0.6, 1.8)
+    f = ParticleFilter(P, (100.0, 90.0, 1.0), std, srange, seed, DEV, frame_size=(224, 224), lam=20.0, weight_bits=40)
+    ref = np.empty((3, P), np.float32)
+    ref[0], ref[1], ref[2] = 100.0, 90.0, 1.0
+    rng = np.random.default_rng(5)
+    t = rng.standard_normal(D).astype(np.float32)
+    t /= np.linalg.norm(t)
+    for k in range(1, 6):
+        f.predict()
+        pf.predict(ref, 0, seed, k, std, 224, 224, srange)
+        assert np.array_equal(f.particles.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"frame {k}: predict"
+        assert f.states.shape == (P, 3) and torch.equal(f.states.cpu(), torch.from_numpy(ref.T.copy()))
+        feat = (rng.standard_normal((P, D)) + 2.0 * t).astype(np.float32)
+        Q = f.update(torch.from_numpy(feat).to(DEV), torch.from_numpy(t).to(DEV)).cpu().numpy()
+        sim = torch.empty(P, device=DEV)
+        vpf().cosine_weight(torch.from_numpy(feat).to(DEV), torch.from_numpy(t).to(DEV), 20.0, 40,
+                            torch.empty(P, device=DEV, dtype=torch.int64), sim)
+        s = sim.cpu().numpy()
+        cos = feat.astype(np.float64) @ t / np.linalg.norm(feat.astype(np.float64), axis=1)
+        np.testing.assert_allclose(s, cos, atol=1e-5)
+        assert np.array_equal(Q, pf.weights_to_Q(s, 20.0, 40)), f"frame {k}: Q"
+        est = f.estimate()
+        np.testing.assert_allclose(est, pf.estimate(Q, ref), rtol=1e-12)
+        anc = f.resample().cpu().numpy()
+        anc_ref = pf.resample(Q, pf.resample_U(seed, k))
+        assert np.array_equal(anc, anc_ref), f"frame {k}: ancestors"
+        ref = np.ascontiguousarray(ref[:, anc_ref])
+        assert np.array_equal(f.particles.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"frame {k}: states"

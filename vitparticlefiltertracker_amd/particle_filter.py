@@ -202,6 +202,12 @@ class ParticleFilter:
         self.reset(init_state)
 
     # ------------------------------------------------------------------ state
+    @property
+    def states(self) -> torch.Tensor:
+        """The particles as float32[P_local][3] rows (x, y, scale): a transposed VIEW of the SoA `particles`
+        (SURVEY.md §8b's [P, 3] shape); writes through it land in the filter's state."""
+        return self.particles.t()
+
     def reset(self, state) -> None:
         x, y, s = (float(v) for v in state)
         self.particles[0].fill_(x)
