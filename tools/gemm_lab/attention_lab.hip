@@ -605,206 +605,235 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int NT = NP >> 5;              // 32-key chunks
     char* Ks = smem;
     char* Vs = smem + NP * ROWB;
-    const int bh = blockIdx.x;
-    const int b = bh / H, h = bh - (bh / H) * H;
-    const int D = H * HD;
-    const int64_t row0 = (int64_t)b * N;
-    const bf16_t* qbase = qkv + row0 * 3 * D + h * HD;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int l32 = lane & 31, hh = lane >> 5;
-    const int nstrips = (q_rows + 31) >> 5;
-    // wave-uniform: this wave's strip holds query N - 1 and at most 16 real queries. Decided by N, not q_rows, so a
-    // row's result does not depend on how many rows the call computes.
-    const int nlast = (N - 1) >> 5;
-    const bool w16 = TAIL16 && !OUT8 && wid == nlast && wid < nstrips && N - 32 * nlast <= 16;
-
-    if constexpr (LAB == 3) {   // lab: the second resident workgroup of each CU starts ld8 x ~4k cycles late
-        if (bh >= 256 && bh < 512)
-            for (int i = 0; i < ld8; ++i) __builtin_amdgcn_s_sleep(64);
-    }
-    const int q = wid * 32 + l32;
-    // Q fragments by inline-asm loads: hipcc does not count them, so it cannot merge them into a vmcnt(0) at
-    // the first MFMA (which would also drain every K/V chunk). They are older than all DMA pieces, so the
-    // first chunk's counted wait retires them; the empty asm after it pins every use below that wait.
-    // 16-query strip: qf[kk] (kk < 2) = Q[32 wid + lane % 16][32 kk + 8 (lane / 16) ..] (attn_step16's B operand;
-    // qf[2], qf[3] re-read the same bytes and are unused).
-    // One asm load statement per register for both strip kinds, with the strip kind in the address only: loads issued
-    // in two branches would leave each qf a phi of two asm outputs, and the copies that resolve it run at the branch
-    // merge, before the loads land, so the registers the MFMAs read were stale (the NaNs of round 2's 16-query tail,
-    // on the 32-query strips too).
-    bf16x8 qf[4];
-    {
-        const bf16_t* qp = w16 ? qbase + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
-                               : qbase + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
-        const int step = w16 ? 32 : 16;
-        if constexpr (LAB == 1) {
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) qf[ks] = bf16x8{(short)(lane + ks), 0x3c00, 0x3c00, 0x3c00, 0, 0, 0, (short)wid};
-        } else {
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + (w16 ? (ks & 1) : ks) * step));
+    // LAB 7 (round 4 s2): persistent (gridDim = 2 x CUs, workgroup w takes units w, w + G, ..., lds8 = B H units), and
+    // the second workgroup to start on each CU (a per-CU ticket from HW_ID / XCC_ID, s8 = zeroed int tickets) sleeps ld8
+    // x ~8k cycles once, so the two resident workgroups run their load and compute phases half a unit apart for good
+    auto unit = [&](const int bh) {
+        const int b = bh / H, h = bh - (bh / H) * H;
+        const int D = H * HD;
+        const int64_t row0 = (int64_t)b * N;
+        const bf16_t* qbase = qkv + row0 * 3 * D + h * HD;
+        // LAB 7: the lane id re-read through an opaque asm per unit, so nothing lane-derived is hoisted out of the unit
+        // loop (hoisted, it spilled 48 VGPRs)
+        int lane_id = (int)(threadIdx.x & 63);
+        if constexpr (LAB == 7) asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_id));
+        const int tid = (int)(threadIdx.x & ~63u) + lane_id, lane = lane_id;
+        const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int l32 = lane & 31, hh = lane >> 5;
+        const int nstrips = (q_rows + 31) >> 5;
+        // wave-uniform: this wave's strip holds query N - 1 and at most 16 real queries. Decided by N, not q_rows, so a
+        // row's result does not depend on how many rows the call computes.
+        const int nlast = (N - 1) >> 5;
+        const bool w16 = TAIL16 && !OUT8 && wid == nlast && wid < nstrips && N - 32 * nlast <= 16;
+    
+        if constexpr (LAB == 3) {   // lab: the second resident workgroup of each CU starts ld8 x ~4k cycles late
+            if (bh >= 256 && bh < 512)
+                for (int i = 0; i < ld8; ++i) __builtin_amdgcn_s_sleep(64);
         }
-    }
-    if constexpr (LAB != 1) {
-        const bool isv = wid >= 4;
-        const int sub = lane >> 3, slot = lane & 7;
-        const bf16_t* src0 = qbase + (isv ? 2 * D : D);
-        char* img = isv ? Vs : Ks;
-        for (int c = 0; c < NT; ++c) {
-            const int g = c * 4 + (wid & 3);                 // 8-row piece index inside the image
-            const int r = 8 * g + sub;
-            const int ch = isv ? (slot ^ (((r >> 1) & 1) << 2)) : (slot ^ ((r >> 1) & 7));
-            __builtin_amdgcn_global_load_lds((gptr_t)(src0 + (int64_t)min(r, N - 1) * 3 * D + ch * 8),
-                                             (lptr_t)(img + g * 1024), 16, 0, 0);
+        const int q = wid * 32 + l32;
+        // Q fragments by inline-asm loads: hipcc does not count them, so it cannot merge them into a vmcnt(0) at
+        // the first MFMA (which would also drain every K/V chunk). They are older than all DMA pieces, so the
+        // first chunk's counted wait retires them; the empty asm after it pins every use below that wait.
+        // 16-query strip: qf[kk] (kk < 2) = Q[32 wid + lane % 16][32 kk + 8 (lane / 16) ..] (attn_step16's B operand;
+        // qf[2], qf[3] re-read the same bytes and are unused).
+        // One asm load statement per register for both strip kinds, with the strip kind in the address only: loads issued
+        // in two branches would leave each qf a phi of two asm outputs, and the copies that resolve it run at the branch
+        // merge, before the loads land, so the registers the MFMAs read were stale (the NaNs of round 2's 16-query tail,
+        // on the 32-query strips too).
+        bf16x8 qf[4];
+        {
+            const bf16_t* qp = w16 ? qbase + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
+                                   : qbase + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
+            const int step = w16 ? 32 : 16;
+            if constexpr (LAB == 1) {
+    #pragma unroll
+                for (int ks = 0; ks < 4; ++ks) qf[ks] = bf16x8{(short)(lane + ks), 0x3c00, 0x3c00, 0x3c00, 0, 0, 0, (short)wid};
+            } else {
+    #pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + (w16 ? (ks & 1) : ks) * step));
+            }
         }
-    }
-    // The Q loads are older than this wave's NT DMA pieces: landed once at most NT are outstanding. Wait and pin the
-    // registers HERE, before the strip-kind branch: the compiler copies asm-load destinations wherever register
-    // allocation wants (the phi / live-range copies of the w16 branch below moved qf before any wait, reading stale
-    // registers: the round-2 NaN). The first chunk barrier waits for CPB chunks, so this costs nothing.
-    wait_vmcnt(NT);
-    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
-    const bool active = LAB != 2 && wid < nstrips;
-    constexpr bool SWP = LAB == 6;   // lab: the software-pipelined 32-query strip (VPF_ATTN_LAB=5)
-    const int nfull = N >> 5;             // chunks without padded keys
-    // The chunk loop, one template for both strip kinds: the barrier schedule (a counted wait + s_barrier before
-    // chunks 0, CPB, 2 CPB, ..., and before the padded tail chunk) depends on N and CPB only.
-    auto run_strip = [&](auto k16, f32x16& o0, f32x16& o1, f32x4 (&o16)[4], float& m, float& l) {
-        constexpr bool W16 = decltype(k16)::value;
-        auto pin_q = [&]() {
-            if constexpr (W16) asm volatile("" : "+v"(qf[0]), "+v"(qf[1]) :: "memory");
-            else asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
-        };
-        if constexpr (!W16 && SWP) {
-            // software-pipelined 32-query strip: the barrier before chunk group g (chunks g CPB ..) is taken before
-            // QK^T of chunk g CPB, i.e. in iteration g CPB - 1; the same barriers in the same order as below
-            if (!active) {   // a wave without a strip passes the same barriers
-                for (int c = 0; c < NT; c += CPB) {
-                    wait_vmcnt(max(NT - c - CPB, 0));
-                    __builtin_amdgcn_s_barrier();
+        if constexpr (LAB != 1) {
+            const bool isv = wid >= 4;
+            const int sub = lane >> 3, slot = lane & 7;
+            const bf16_t* src0 = qbase + (isv ? 2 * D : D);
+            char* img = isv ? Vs : Ks;
+            for (int c = 0; c < NT; ++c) {
+                const int g = c * 4 + (wid & 3);                 // 8-row piece index inside the image
+                const int r = 8 * g + sub;
+                const int ch = isv ? (slot ^ (((r >> 1) & 1) << 2)) : (slot ^ ((r >> 1) & 7));
+                __builtin_amdgcn_global_load_lds((gptr_t)(src0 + (int64_t)min(r, N - 1) * 3 * D + ch * 8),
+                                                 (lptr_t)(img + g * 1024), 16, 0, 0);
+            }
+        }
+        // The Q loads are older than this wave's NT DMA pieces: landed once at most NT are outstanding. Wait and pin the
+        // registers HERE, before the strip-kind branch: the compiler copies asm-load destinations wherever register
+        // allocation wants (the phi / live-range copies of the w16 branch below moved qf before any wait, reading stale
+        // registers: the round-2 NaN). The first chunk barrier waits for CPB chunks, so this costs nothing.
+        wait_vmcnt(NT);
+        asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        const bool active = LAB != 2 && wid < nstrips;
+        constexpr bool SWP = LAB == 6;   // lab: the software-pipelined 32-query strip (VPF_ATTN_LAB=5)
+        const int nfull = N >> 5;             // chunks without padded keys
+        // The chunk loop, one template for both strip kinds: the barrier schedule (a counted wait + s_barrier before
+        // chunks 0, CPB, 2 CPB, ..., and before the padded tail chunk) depends on N and CPB only.
+        auto run_strip = [&](auto k16, f32x16& o0, f32x16& o1, f32x4 (&o16)[4], float& m, float& l) {
+            constexpr bool W16 = decltype(k16)::value;
+            auto pin_q = [&]() {
+                if constexpr (W16) asm volatile("" : "+v"(qf[0]), "+v"(qf[1]) :: "memory");
+                else asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+            };
+            if constexpr (!W16 && SWP) {
+                // software-pipelined 32-query strip: the barrier before chunk group g (chunks g CPB ..) is taken before
+                // QK^T of chunk g CPB, i.e. in iteration g CPB - 1; the same barriers in the same order as below
+                if (!active) {   // a wave without a strip passes the same barriers
+                    for (int c = 0; c < NT; c += CPB) {
+                        wait_vmcnt(max(NT - c - CPB, 0));
+                        __builtin_amdgcn_s_barrier();
+                    }
+                    return;
+                }
+                wait_vmcnt(max(NT - CPB, 0));
+                __builtin_amdgcn_s_barrier();
+                pin_q();
+                // full chunks c < nfull; the tail chunk (c = nfull < NT) is peeled. (Unrolled by two, to alternate the
+                // score tiles without the 8 v_mov_b64 of `cur = nxt`, hipcc spills 20-75 VGPRs at the 128 limit.)
+                f32x16 cur = attn_qk32(Ks, 0, lane, qf);
+                for (int c = 0; c < nfull; ++c) {
+                    f32x16 nxt;
+                    if (c + 1 < NT) {
+                        if ((c + 1) % CPB == 0) {
+                            wait_vmcnt(max(NT - (c + 1) - CPB, 0));
+                            __builtin_amdgcn_s_barrier();
+                            pin_q();
+                        }
+                        nxt = attn_qk32(Ks, (c + 1) * 32, lane, qf);
+                    }
+                    attn_sm_pv32<0>(Vs, c * 32, N, lane, cur, scale_log2, m, l, o0, o1);
+                    cur = nxt;
+                }
+                if (nfull < NT) {
+                    if (TAIL8 && N - nfull * 32 <= 8) attn_sm_pv32<2>(Vs, nfull * 32, N, lane, cur, scale_log2, m, l, o0, o1);
+                    else attn_sm_pv32<1>(Vs, nfull * 32, N, lane, cur, scale_log2, m, l, o0, o1);
                 }
                 return;
             }
-            wait_vmcnt(max(NT - CPB, 0));
-            __builtin_amdgcn_s_barrier();
-            pin_q();
-            // full chunks c < nfull; the tail chunk (c = nfull < NT) is peeled. (Unrolled by two, to alternate the
-            // score tiles without the 8 v_mov_b64 of `cur = nxt`, hipcc spills 20-75 VGPRs at the 128 limit.)
-            f32x16 cur = attn_qk32(Ks, 0, lane, qf);
-            for (int c = 0; c < nfull; ++c) {
-                f32x16 nxt;
-                if (c + 1 < NT) {
-                    if ((c + 1) % CPB == 0) {
-                        wait_vmcnt(max(NT - (c + 1) - CPB, 0));
-                        __builtin_amdgcn_s_barrier();
-                        pin_q();
-                    }
-                    nxt = attn_qk32(Ks, (c + 1) * 32, lane, qf);
+            int c = 0;
+            for (; c < nfull; ++c) {
+                if (c % CPB == 0) {   // chunks c .. c+CPB-1 landed for every wave
+                    wait_vmcnt(max(NT - c - CPB, 0));
+                    __builtin_amdgcn_s_barrier();
+                    pin_q();
                 }
-                attn_sm_pv32<0>(Vs, c * 32, N, lane, cur, scale_log2, m, l, o0, o1);
-                cur = nxt;
+                if (active) {
+                    if constexpr (W16) attn_step16<false>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
+                    else attn_step<1, false, true, LAB != 5>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                }
             }
-            if (nfull < NT) {
-                if (TAIL8 && N - nfull * 32 <= 8) attn_sm_pv32<2>(Vs, nfull * 32, N, lane, cur, scale_log2, m, l, o0, o1);
-                else attn_sm_pv32<1>(Vs, nfull * 32, N, lane, cur, scale_log2, m, l, o0, o1);
+            if (c < NT) {
+                if (c % CPB == 0) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    pin_q();
+                }
+                if (active) {
+                    if constexpr (W16) attn_step16<true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
+                    else if (TAIL8 && N - c * 32 <= 8) attn_step_tail8(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                    else attn_step<1, true, true, LAB != 5>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                }
+            }
+        };
+        float m = -INFINITY, l = 0.f;
+        if (w16) {
+            f32x16 o0 = {}, o1 = {};
+            f32x4 o16[4] = {};
+            run_strip(std::true_type{}, o0, o1, o16, m, l);
+            // the 4 lanes lane % 16 + 16 g share query 32 wid + lane % 16; lane holds dims 16 dt + 4g .. +3
+            l = xor32_sum(xor16_sum(l));
+            const float inv = 1.0f / l;
+            const int qq = wid * 32 + (lane & 15);
+            if (qq < q_rows) {
+                bf16_t* orow = out + (row0 + qq) * D + h * HD + 4 * (lane >> 4);
+    #pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+                    *reinterpret_cast<uint2*>(orow + 16 * dt) = make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
+                                                                          pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
             }
             return;
         }
-        int c = 0;
-        for (; c < nfull; ++c) {
-            if (c % CPB == 0) {   // chunks c .. c+CPB-1 landed for every wave
-                wait_vmcnt(max(NT - c - CPB, 0));
-                __builtin_amdgcn_s_barrier();
-                pin_q();
-            }
-            if (active) {
-                if constexpr (W16) attn_step16<false>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
-                else attn_step<1, false, true, LAB != 5>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-            }
-        }
-        if (c < NT) {
-            if (c % CPB == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-                pin_q();
-            }
-            if (active) {
-                if constexpr (W16) attn_step16<true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
-                else if (TAIL8 && N - c * 32 <= 8) attn_step_tail8(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-                else attn_step<1, true, true, LAB != 5>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-            }
-        }
-    };
-    float m = -INFINITY, l = 0.f;
-    if (w16) {
         f32x16 o0 = {}, o1 = {};
-        f32x4 o16[4] = {};
-        run_strip(std::true_type{}, o0, o1, o16, m, l);
-        // the 4 lanes lane % 16 + 16 g share query 32 wid + lane % 16; lane holds dims 16 dt + 4g .. +3
-        l = xor32_sum(xor16_sum(l));
+        f32x4 o16_unused[4];
+        run_strip(std::false_type{}, o0, o1, o16_unused, m, l);
+        if (!active) return;
+        l = xor32_sum(l);
         const float inv = 1.0f / l;
-        const int qq = wid * 32 + (lane & 15);
-        if (qq < q_rows) {
-            bf16_t* orow = out + (row0 + qq) * D + h * HD + 4 * (lane >> 4);
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-                *reinterpret_cast<uint2*>(orow + 16 * dt) = make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
-                                                                      pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
+        // Lane (l32, hh) holds dims 8k + 4hh .. +3 of query l32 for the eight 8-dim groups k (o0: k < 4, o1: k >= 4).
+        // v_permlane32_swap per pair (k, k+1) gives the lower half-wave dims 8k..8k+7 and the upper half-wave
+        // 8k+8..8k+15: one 16-B store per pair (cdna_hip_programming.md T21) instead of two 8-B stores.
+        uint32_t gx[8], gy[8];
+    #pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const f32x16& o = k < 4 ? o0 : o1;
+            const int b4 = 4 * (k & 3);
+            gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
+            gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
         }
-        return;
-    }
-    f32x16 o0 = {}, o1 = {};
-    f32x4 o16_unused[4];
-    run_strip(std::false_type{}, o0, o1, o16_unused, m, l);
-    if (!active) return;
-    l = xor32_sum(l);
-    const float inv = 1.0f / l;
-    // Lane (l32, hh) holds dims 8k + 4hh .. +3 of query l32 for the eight 8-dim groups k (o0: k < 4, o1: k >= 4).
-    // v_permlane32_swap per pair (k, k+1) gives the lower half-wave dims 8k..8k+7 and the upper half-wave
-    // 8k+8..8k+15: one 16-B store per pair (cdna_hip_programming.md T21) instead of two 8-B stores.
-    uint32_t gx[8], gy[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const f32x16& o = k < 4 ? o0 : o1;
-        const int b4 = 4 * (k & 3);
-        gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
-        gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
-    }
-    uint4 ov[4];
-#pragma unroll
-    for (int k = 0; k < 8; k += 2) {   // all lanes active: the swaps read the partner half-wave
-        const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
-        const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
-        ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
-    }
-    if constexpr (OUT8) {
-        // lane (l32, hh) holds dims 16k + 8hh .. +7 (k = 0..3): block b = dims 32b .. 32b+31 is ov[2b], ov[2b+1]
-        // of this lane and of its partner lane l32 + 32 (1 - hh)
-        int E[2];
-#pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2) {
-            uint32_t am = max(mx8_amax8(ov[2 * b2]), mx8_amax8(ov[2 * b2 + 1]));
-            {
-                const auto r = __builtin_amdgcn_permlane32_swap(am, am, false, false);
-                am = max(r[0], r[1]);
+        uint4 ov[4];
+    #pragma unroll
+        for (int k = 0; k < 8; k += 2) {   // all lanes active: the swaps read the partner half-wave
+            const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
+            const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
+            ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+        }
+        if constexpr (OUT8) {
+            // lane (l32, hh) holds dims 16k + 8hh .. +7 (k = 0..3): block b = dims 32b .. 32b+31 is ov[2b], ov[2b+1]
+            // of this lane and of its partner lane l32 + 32 (1 - hh)
+            int E[2];
+    #pragma unroll
+            for (int b2 = 0; b2 < 2; ++b2) {
+                uint32_t am = max(mx8_amax8(ov[2 * b2]), mx8_amax8(ov[2 * b2 + 1]));
+                {
+                    const auto r = __builtin_amdgcn_permlane32_swap(am, am, false, false);
+                    am = max(r[0], r[1]);
+                }
+                E[b2] = mx8_block_exp(am);
             }
-            E[b2] = mx8_block_exp(am);
+            if (q < q_rows) {
+                const int64_t r = row0 + q;
+                uint8_t* orow = out8 + r * ld8 + h * HD + 8 * hh;
+    #pragma unroll
+                for (int k = 0; k < 4; ++k) *reinterpret_cast<uint2*>(orow + 16 * k) = mx8_pack8(ov[k], E[k >> 1]);
+                s8[mx8_scale_byte(r, h * HD + 32 * hh, lds8)] = (uint8_t)(E[hh] + 127);
+            }
+            return;
         }
         if (q < q_rows) {
-            const int64_t r = row0 + q;
-            uint8_t* orow = out8 + r * ld8 + h * HD + 8 * hh;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) *reinterpret_cast<uint2*>(orow + 16 * k) = mx8_pack8(ov[k], E[k >> 1]);
-            s8[mx8_scale_byte(r, h * HD + 32 * hh, lds8)] = (uint8_t)(E[hh] + 127);
+            bf16_t* orow = out + (row0 + q) * D + h * HD + 8 * hh;
+    #pragma unroll
+            for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
         }
-        return;
-    }
-    if (q < q_rows) {
-        bf16_t* orow = out + (row0 + q) * D + h * HD + 8 * hh;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
+    };
+    if constexpr (LAB == 7) {
+        if (threadIdx.x == 0) {
+            const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804);    // HW_REG_HW_ID: cu 11:8, sh 12, se 15:13
+            const uint32_t xcc = __builtin_amdgcn_s_getreg(0xF814);   // HW_REG_XCC_ID
+            const int slot = (int)(((xcc & 7) << 8) | ((hw >> 8) & 0xFF));
+            const int t = atomicAdd(reinterpret_cast<int*>(s8) + slot, 1);
+            *reinterpret_cast<volatile int*>(smem) = t;
+        }
+        __syncthreads();
+        const int ticket = *reinterpret_cast<volatile int*>(smem);
+        __syncthreads();
+        if (ticket & 1)
+            for (int i = 0; i < ld8; ++i) __builtin_amdgcn_s_sleep(127);
+        for (int u = blockIdx.x; u < lds8; u += gridDim.x) {
+            unit(u);
+            __builtin_amdgcn_s_waitcnt(0);   // this unit's stores / DMAs retired; every wave is done with the image
+            __builtin_amdgcn_s_barrier();
+        }
+    } else {
+        unit(blockIdx.x);
     }
 }
 
@@ -1206,7 +1235,7 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
         return VPF_ERR_ARG;
     if (B == 0) return 0;
     const int NP = (N + 31) & ~31;
-    const size_t lds = (size_t)NP * ROWB * 2;
+    size_t lds = (size_t)NP * ROWB * 2;
     const float scale_log2 = scale * 1.44269504088896341f;
     const int strips = (q_rows + 31) / 32;
     const int64_t BH = B * H;
@@ -1252,18 +1281,39 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
         int lab_arg = 0;
 #ifdef VPF_GEMM_LAB
         {   // lab builds: VPF_ATTN_LAB=1 compute only, =2 loads only (timing probes, outputs meaningless)
-            static const pipe_fn lab[5] = {k_attn_bf16_pipe<PIPE_CPB, false, true, true, 1>,
+            static const pipe_fn lab[6] = {k_attn_bf16_pipe<PIPE_CPB, false, true, true, 1>,
                                            k_attn_bf16_pipe<PIPE_CPB, false, true, true, 2>,
                                            k_attn_bf16_pipe<PIPE_CPB, false, true, true, 3>,
                                            k_attn_bf16_pipe<PIPE_CPB, false, true, true, 5>,
-                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 6>};
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 6>,
+                                           k_attn_bf16_pipe<PIPE_CPB, false, true, true, 7>};
             const char* le = getenv("VPF_ATTN_LAB");
-            if (le && le[0] >= '1' && le[0] <= '5') {
+            if (le && le[0] >= '1' && le[0] <= '6') {
                 fn = lab[le[0] - '1'];
                 (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             }
-            const char* st = getenv("VPF_ATTN_STAGGER");   // LAB 3's sleep count
+            const char* st = getenv("VPF_ATTN_STAGGER");   // LAB 3's / LAB 7's sleep count
             lab_arg = st ? atoi(st) : 0;
+            if (le && le[0] == '6') {   // LAB 7: persistent grid of 2 workgroups per CU, per-CU tickets zeroed
+                static int* tickets = nullptr;
+                static int cus = 0;
+                if (!tickets) {
+                    if (hipMalloc((void**)&tickets, 2048 * sizeof(int)) != hipSuccess) return VPF_ERR_ARG;
+                    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+                }
+                (void)hipMemsetAsync(tickets, 0, 2048 * sizeof(int), (hipStream_t)stream);
+                hipLaunchKernelGGL(fn, dim3((unsigned)(2 * cus)), dim3(512), lds, (hipStream_t)stream, qkv,
+                                   reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows, (uint8_t*)nullptr, lab_arg,
+                                   reinterpret_cast<uint8_t*>(tickets), (int)(B * H));
+                VPF_RETURN_LAUNCH();
+            }
+            // round 4 s2: VPF_ATTN_LDS=<bytes> raises the dynamic LDS request (e.g. 100000: one workgroup per CU) to time
+            // the kernel and its compute-only / load-only probes at one resident workgroup instead of two
+            const char* lp = getenv("VPF_ATTN_LDS");
+            if (lp && (size_t)atoi(lp) > lds) {
+                lds = (size_t)atoi(lp);
+                (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            }
         }
 #endif
         hipLaunchKernelGGL(fn, dim3((unsigned)(B * H)), dim3(512), lds, (hipStream_t)stream, qkv,
