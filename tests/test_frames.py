@@ -167,3 +167,25 @@ def test_pillow_images_and_directory(tmp_path):
     np.testing.assert_array_equal(out[3], clip[3])
     np.testing.assert_array_equal(out[4], np.repeat(grey[..., None], 3, 2))
     np.testing.assert_array_equal(next(fr.iter_frames(str(d / "f000.png"))), clip[0])
+
+
+def test_animated_gif_and_multipage_tiff(tmp_path):
+    """An animated GIF (palette: lossy on noise, exact on a few flat colours) and a multi-page TIFF (lossless) read as
+    clips, every frame in order."""
+    from PIL import Image
+    clip = _clip(4)
+    pages = [Image.fromarray(f, "RGB") for f in clip]
+    pages[0].save(tmp_path / "clip.tif", save_all=True, append_images=pages[1:])
+    out = list(fr.iter_frames(str(tmp_path / "clip.tif")))
+    assert len(out) == 4
+    for k in range(4):
+        np.testing.assert_array_equal(out[k], clip[k])
+    flat = np.zeros((4, 20, 30, 3), np.uint8)
+    for k in range(4):
+        flat[k, :, : 10 + 5 * k] = (255, 0, 0)          # a growing red bar on black
+    gif = [Image.fromarray(f, "RGB") for f in flat]
+    gif[0].save(tmp_path / "clip.gif", save_all=True, append_images=gif[1:], duration=40, loop=0)
+    out = list(fr.iter_frames(str(tmp_path / "clip.gif")))
+    assert len(out) == 4
+    for k in range(4):
+        np.testing.assert_array_equal(out[k], flat[k])

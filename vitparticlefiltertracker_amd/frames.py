@@ -269,6 +269,15 @@ def read_image_pil(path) -> np.ndarray:
         return np.ascontiguousarray(np.asarray(im.convert("RGB"), dtype=np.uint8))
 
 
+def read_sequence_pil(path) -> Iterator[np.ndarray]:
+    """Every frame of a multi-frame Pillow file (animated GIF / WebP / PNG, multi-page TIFF) as uint8[H][W][3] RGB;
+    a single-frame image yields one frame."""
+    with _pil().open(path) as im:
+        for k in range(int(getattr(im, "n_frames", 1))):
+            im.seek(k)
+            yield np.ascontiguousarray(np.asarray(im.convert("RGB"), dtype=np.uint8))
+
+
 def write_image_pil(path, rgb: np.ndarray, quality: int = 95) -> None:
     """Write uint8[H][W][3] RGB in the format the file suffix names (PNG lossless; JPEG at `quality`)."""
     im = _pil().fromarray(np.ascontiguousarray(rgb, dtype=np.uint8), "RGB")
@@ -293,7 +302,8 @@ def _read_image(p) -> np.ndarray:
 
 def iter_frames(source) -> Iterator[np.ndarray]:
     """Yield uint8[H][W][3] frames from a clip array, a `.npy` clip, a `.y4m` video, a single image (PPM/PGM, or
-    PNG / JPEG / BMP / TIFF / WebP through Pillow), or a directory of such frames (sorted by name)."""
+    PNG / JPEG / BMP / TIFF / WebP through Pillow; an animated GIF / WebP / PNG or a multi-page TIFF yields all its
+    frames), or a directory of single-image frames (sorted by name)."""
     if isinstance(source, np.ndarray):
         arr = source if source.ndim == 4 else source[None]
         for f in arr:
@@ -312,8 +322,8 @@ def iter_frames(source) -> Iterator[np.ndarray]:
     if low.endswith((".ppm", ".pgm", ".pnm")):
         yield read_pnm(path)
         return
-    if low.endswith(_PIL_EXT):
-        yield read_image_pil(path)
+    if low.endswith(_PIL_EXT + (".gif",)):   # a single image, or every frame of an animated / multi-page file
+        yield from read_sequence_pil(path)
         return
     arr = np.load(path, mmap_mode="r", allow_pickle=False)
     for f in (arr if arr.ndim == 4 else arr[None]):
