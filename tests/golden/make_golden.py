@@ -9,7 +9,7 @@ perturbed biases / LayerNorm affines so every term is exercised) into ViTModel, 
 pixel tensors, and stores inputs' seeds plus CLS features (final LN) and per-layer hidden-state
 statistics. Weights and pixels are regenerated from their seeds by the tests; only outputs are stored.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [case names]
 """
 from __future__ import annotations
 
@@ -29,6 +29,7 @@ CASES = [
     # (arch, weight seed, pixel seed, batch)
     ("vit_tiny_patch16_224", 11, 101, 4),
     ("vit_base_patch16_224", 12, 102, 1),
+    ("vit_large_patch14_336", 13, 103, 1),   # round 4 s2: configs[3]'s architecture (N = 577, D = 1024, 24 blocks)
 ]
 
 
@@ -76,7 +77,10 @@ def hf_model(arch, w):
 @torch.no_grad()
 def main() -> None:
     import transformers
+    only = set(sys.argv[1:])   # optional: the case names to (re)generate
     for name, wseed, pseed, batch in CASES:
+        if only and name not in only:
+            continue
         arch = ARCHS[name]
         w = make_vit_weights(arch, seed=wseed, perturb_affine=True)
         m = hf_model(arch, w)

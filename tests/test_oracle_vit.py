@@ -19,7 +19,7 @@ def pixels_for(seed: int, batch: int, size: int) -> torch.Tensor:
     return torch.rand(batch, 3, size, size, generator=g) * 2.0 - 1.0
 
 
-@pytest.mark.parametrize("name", ["vit_tiny_patch16_224", "vit_base_patch16_224"])
+@pytest.mark.parametrize("name", ["vit_tiny_patch16_224", "vit_base_patch16_224", "vit_large_patch14_336"])
 def test_vit_oracle_matches_transformers_golden(name):
     d = np.load(os.path.join(GOLD, f"vit_{name}.npz"), allow_pickle=False)
     arch = ARCHS[name]
