@@ -106,6 +106,9 @@ for step in "$@"; do
     bench8)
       timeout -k 10 900 python bench.py --dtype fp8 --steps 5 --warmup 2 --cpu-baseline off > $OUT/bench8.log 2>&1
       ok_or_stop $? bench8; tail -1 $OUT/bench8.log | cut -c1-600 ;;
+    libab)   # same-process A/B of the product library against LIBAB_LIB (default ab_libs/libvpf_direct.so)
+      timeout -k 10 600 python tools/lib_ab.py ${LIBAB_ROUNDS:-7} ${LIBAB_CASES:-bf16_qkv,bf16_proj,bf16_fc1,bf16_fc2} ${LIBAB_LIB:-ab_libs/libvpf_direct.so} > $OUT/lib_ab.log 2>&1
+      ok_or_stop $? libab; grep -v amdgpu.ids $OUT/lib_ab.log ;;
     lab)
       timeout -k 10 600 tools/gemm_lab/gemm_lab 5 "$LAB_SHAPES" "$LAB_VARS" 1 > $OUT/lab.log 2>&1
       ok_or_stop $? lab; grep -v "inf TFLOP" $OUT/lab.log | tail -40 ;;

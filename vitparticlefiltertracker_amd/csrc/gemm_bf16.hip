@@ -66,6 +66,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
 
     int m0, n0;
     tile_of(M, N, group, m0, n0);   // XCD-aware grouped tile order (gemm_common.h)
+    // the GELU epilogues store straight from the accumulators (store_wave_tile_direct: W rows permuted in the DMA)
+    constexpr bool DIRECT = (EPI == VPF_EPI_LN_GELU || EPI == VPF_EPI_BIAS_GELU) && !OUT8 && !PART;
 
     // ---- per-lane DMA source offsets (bytes, relative to the block's panel base) ----
     const int kbase = PART ? (int)blockIdx.y * (K / (int)gridDim.y) : 0;   // PART: this split's first K column
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         const int pch = lane & 7;
         const int lch = pch ^ ((row >> 1) & 7);    // logical chunk stored at this physical slot
         const int ra = min(row, M - 1 - m0);
-        const int rb = min(row, N - 1 - n0);
+        const int rb = min(DIRECT ? wperm(row) : row, N - 1 - n0);
         offA[i] = (uint32_t)ra * (uint32_t)(lda * 2) + (uint32_t)(lch * 16);
         offB[i] = (uint32_t)rb * (uint32_t)(K * 2) + (uint32_t)(lch * 16);
     }
@@ -251,6 +253,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     uint4 res[16];
     constexpr bool PIPE = EPI != VPF_EPI_PATCH && !OUT8;
+    if constexpr (DIRECT) {
+        if constexpr (LN) {   // the LN combine above is read by the other waves
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        store_wave_tile_direct<EPI>(aux, acc, wm, wn, m0, n0, lane, C, ldc, M, N);
+        return;
+    }
     if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual<PIPE>(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
     // every wave is done with the operand ring (reused as 8 x 16 KiB images) and the LN combine is visible; a raw
     // barrier, so the residual loads stay in flight across it (no DMA is outstanding after the K loop)
@@ -311,6 +322,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_pp(const bf16_t* __restrict__
 
     int m0, n0;
     tile_of(M, N, group, m0, n0);
+    constexpr bool DIRECT = (EPI == VPF_EPI_LN_GELU || EPI == VPF_EPI_BIAS_GELU) && !OUT8;
 
     const char* Ablk = reinterpret_cast<const char*>(A) + (size_t)m0 * lda * 2;
     const char* Bblk = reinterpret_cast<const char*>(W) + (size_t)n0 * K * 2;
@@ -321,7 +333,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_pp(const bf16_t* __restrict__
         const int rho = (wid + 8 * p) * 8 + (lane >> 3);             // local row 0..127
         const int lch = (lane & 7) ^ ((rho >> 1) & 7);               // logical chunk at this physical slot
         const int ra0 = (rho >> 6) * 128 + (rho & 63);               // A0: g*128 + r
-        const int rb0 = (rho >> 5) * 64 + (rho & 31);                // B0: wn*64 + r
+        const int rb0 = (rho >> 5) * 64 + (DIRECT ? wperm(rho & 31) : (rho & 31));   // B0: wn*64 + r
         const int ra[2] = {ra0, ra0 + 64}, rb[2] = {rb0, rb0 + 32};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -466,6 +478,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_pp(const bf16_t* __restrict__
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): nothing outstanding (see k_gemm_bf16)
     uint4 res[16];
     constexpr bool PIPE = EPI != VPF_EPI_PATCH && !OUT8;
+    if constexpr (DIRECT) {
+        if constexpr (LN) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        store_wave_tile_direct<EPI>(aux, acc, wm, wn, m0, n0, lane, C, ldc, M, N);
+        return;
+    }
     if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual<PIPE>(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();

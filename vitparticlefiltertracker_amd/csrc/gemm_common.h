@@ -273,6 +273,73 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
 // The residual rows a lane adds in store_wave_tile (EPI_BIAS_RESIDUAL): 16 x 16 B, all in flight at once. The
 // kernels issue this right after their K loop, before the epilogue barrier (a raw s_barrier, so the loads stay
 // in flight across it), which gives them the LN combine, the barrier and the image writes to land under.
+// Direct-store epilogue (no LDS image) for the GELU epilogues (FC1: EPI_LN_GELU; EPI_BIAS_GELU), bit-identical to
+// store_wave_tile_pipe. The W K-tile is staged with its rows permuted inside each 32-row group: LDS row r of the B tile
+// holds W row wperm(r) of the tile. Fragment j's MFMA row p then is output column (j >> 1)*32 + (p >> 2)*8 + (j & 1)*4 +
+// (p & 3) of the wave's 64, so a lane's acc[2h][i] and acc[2h+1][i] are the 8 consecutive columns h*32 + fq*8 .. +7 of
+// row i*16 + fr: one 16-B store straight from the accumulators (4 lanes = 64 contiguous bytes of a row, 16 rows per
+// store instruction). The LDS layout and the fragment reads are unchanged (only the DMA source rows move).
+// Measured in one process against the image path (profiles/r4_lab/gemm_direct_store_ab.txt, M = 806,912, outputs
+// bit-identical): FC1 -1.3 %, but QKV +6.9 %, proj +3.3 %, FC2 +0.6 %. A store instruction that covers 16 half rows
+// costs more than one that covers 8 whole rows, which only the VALU-bound GELU epilogue (no LDS image round trip to
+// wait on) more than pays back; a DPP pair exchange that restores 8 whole rows per store costs 16 VALU per row group
+// (QKV +1.2 %, FC1 -0.4 %). So only the GELU epilogues store directly.
+__device__ __forceinline__ int wperm(int r) {
+    return (r & ~31) | (((r >> 2) & 3) << 3) | (((r >> 4) & 1) << 2) | (r & 3);
+}
+
+template <int EPI>
+__device__ __forceinline__ void store_wave_tile_direct(const char* aux, const f32x4 (&acc)[4][8], int wm, int wn, int m0,
+                                                       int n0, int lane, bf16_t* C, int ldc, int M, int N) {
+    static_assert(EPI == VPF_EPI_BIAS_GELU || EPI == VPF_EPI_LN_GELU, "direct stores: the GELU epilogues");
+    constexpr bool LN = EPI == VPF_EPI_LN_GELU;
+    const int fr = lane & 15, fq = lane >> 4;
+    bf16_t* Cl = C + (int64_t)(m0 + wm * 128 + fr) * ldc + (n0 + wn * 64 + fq * 8);
+    float4 bv[4], cv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = (wn * 64 + (j >> 1) * 32 + fq * 8 + (j & 1) * 4) * 4;
+        bv[j] = *reinterpret_cast<const float4*>(aux + c);
+        if constexpr (LN) cv[j] = *reinterpret_cast<const float4*>(aux + 1024 + c);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        f32x2 rsx = {1.f, 1.f}, rsy = {0.f, 0.f};
+        if constexpr (LN) {
+            const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + (wm * 128 + i * 16 + fr) * 8);
+            rsx = f32x2{st.y, st.y};
+            rsy = f32x2{-st.y * st.x, -st.y * st.x};
+        }
+        const int m = m0 + wm * 128 + i * 16 + fr;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int j = 2 * h + k;
+                f32x2 v01, v23;
+                const f32x2 a01 = {acc[j][i][0], acc[j][i][1]}, a23 = {acc[j][i][2], acc[j][i][3]};
+                const f32x2 b01 = {bv[j].x, bv[j].y}, b23 = {bv[j].z, bv[j].w};
+                if constexpr (LN) {
+                    const f32x2 c01 = {cv[j].x, cv[j].y}, c23 = {cv[j].z, cv[j].w};
+                    v01 = __builtin_elementwise_fma(rsx, a01, __builtin_elementwise_fma(rsy, c01, b01));
+                    v23 = __builtin_elementwise_fma(rsx, a23, __builtin_elementwise_fma(rsy, c23, b23));
+                } else {
+                    v01 = a01 + b01;
+                    v23 = a23 + b23;
+                }
+                v01 = gelu_sig2(v01);
+                v23 = gelu_sig2(v23);
+                o[2 * k] = pack_bf2(v01.x, v01.y);
+                o[2 * k + 1] = pack_bf2(v23.x, v23.y);
+            }
+            const int n = n0 + wn * 64 + h * 32 + fq * 8;
+            if (m < M && n < N)
+                *reinterpret_cast<uint4*>(Cl + (int64_t)(i * 16) * ldc + h * 32) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+    }
+}
+
 // PAR: the row order of store_wave_tile_pipe (res[2i + h] = row i*16 + 2*(lane/8) + h), from one per-lane base
 // pointer; !PAR: row it*8 + lane/8 (store_wave_tile).
 template <bool PAR = true>
