@@ -7,7 +7,7 @@ Both count memory-side requests of the L2, Infinity-Cache hits included, i.e. an
 
     python tools/pmc_traffic.py <fetch_dir> <write_dir> [--arch vit_base_patch16_224 --particles 4096 --dtype bf16]
 
-Kernel naming: k_gemm_bf16<4> / k_gemm_mx8<4> = QKV (LN epilogue), <5> = FC1 (LN + GELU), <3> = patch embed, and
+Kernel naming: k_gemm_bf16<4> / k_gemm_pp<4> / k_gemm_mx8<4> = QKV (LN epilogue), <5> = FC1 (LN + GELU), <3> = patch embed, and
 the two full-size <2> (bias + residual) launches of each block alternate proj, FC2 (dispatch order). CLS-row
 launches (grid of one M tile) are skipped. --dtype fp8: the MX8 GEMMs' algorithmic bytes count e4m3 elements
 (1 B) plus one e8m0 scale byte per 32 (configs[4]'s path: QKV / FC1 / FC2 / proj on MX8 operands).
@@ -38,7 +38,7 @@ def load(d, counter):
 def name_gemms(rows, min_grid):
     out, res_toggle = [], 0
     for _, kname, grid, val in rows:
-        tag = "k_gemm_bf16<" if "k_gemm_bf16<" in kname else "k_gemm_mx8<" if "k_gemm_mx8<" in kname else None
+        tag = next((t for t in ("k_gemm_bf16<", "k_gemm_pp<", "k_gemm_mx8<") if t in kname), None)
         if tag is None or grid < min_grid:
             continue
         epi = kname.split(tag)[1].split(">")[0].split(",")[0].strip()

@@ -531,7 +531,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_pp(const bf16_t* __restrict__
 // four-wave AGPR loop, staggered starts, the persistent kernel, the mid-K barrier loop, timing probes) live in the lab
 // build (tools/gemm_lab, libvpf_lab.so); no environment variable selects a kernel here.
 //  * QKV (the LN-folded bias-only epilogue) runs kernel 5: 2.5 % faster there in one process (2.603 vs 2.670 ms,
-//    profiles/r2_gemm_lab/kernel_ab_r2s5.txt); every other epilogue is fastest on kernel 1.
+//    profiles/r2_gemm_lab/kernel_ab_r2s5.txt). FC1 (LN + GELU) runs kernel 5 since its epilogue stores straight from
+//    the accumulators (store_wave_tile_direct): 3.751 vs 3.817 ms (profiles/r4_lab/fc1_direct_kernel_group_ab.txt);
+//    with the LDS-image epilogue the two kernels were level on FC1. Every other epilogue is fastest on kernel 1.
 //  * Tile order (A panels per group; the order never changes a bit), profiles/r2_gemm_lab/group_sweep_r2.txt: the
 //    N <= 1024 GEMMs (proj / FC2: 3 column tiles) are 1-1.5 % faster with 2 panels per group (FC2 3.196 vs 3.226 ms,
 //    proj 1.070 vs 1.082), QKV with 4; FC1 (LN + GELU, 12 column tiles at ViT-B) takes 8: 16 was -0.9 % on FC1 and
@@ -544,7 +546,7 @@ static int g_kernel = 0;   // 0: per-shape default; 1 / 5: forced by vpf_gemm_tu
 static int g_group = -1;   // -1: per-shape default
 static int gemm_kernel_for(int epilogue) {
     if (g_kernel) return g_kernel;
-    return epilogue == VPF_EPI_LN ? 5 : 1;
+    return (epilogue == VPF_EPI_LN || epilogue == VPF_EPI_LN_GELU) ? 5 : 1;
 }
 static int tile_group_for(int64_t N, int epilogue) {
     if (g_group >= 0) return g_group;
