@@ -488,6 +488,65 @@ __device__ __forceinline__ void store_wave_tile(char* img, const char* aux, cons
     }
 }
 
+// fp8-only output straight from the accumulators (gemm_mx8.hip, FC1's LN + GELU epilogue): the MX8 kernel stages the W
+// K-tile with its rows in the order wperm16 (inside each 64-row brick), so fragment j's MFMA row p is output column
+// (p >> 2)*16 + j*4 + (p & 3) of the wave's 64 and a lane's acc[0..3][i] are the 16 consecutive columns fq*16 .. +15 of
+// row i*16 + fr: the 32-column MX block is the lane pair fq, fq ^ 1 (one permlane16_swap), the 16 fp8 elements are one
+// 16-B store (16 rows x 64 B per store instruction, as store_wave_tile_q8), and each lane assembles the scale bytes of
+// its rows in registers (no LDS image). Bit-identical to store_wave_tile_q8.
+__device__ __forceinline__ int wperm16(int r) {
+    return (r & ~63) | (((r >> 2) & 3) << 4) | (((r >> 4) & 3) << 2) | (r & 3);
+}
+
+template <int EPI>
+__device__ __forceinline__ void store_wave_tile_q8_direct(const char* aux, const f32x4 (&acc)[4][8], int wm, int wn,
+                                                          int m0, int n0, int lane, int M, int N, Out8 o8) {
+    static_assert(EPI == VPF_EPI_LN_GELU, "direct fp8 stores: FC1's epilogue");
+    const int fr = lane & 15, fq = lane >> 4;
+    float4 bv[4], cv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = (wn * 64 + fq * 16 + j * 4) * 4;
+        bv[j] = *reinterpret_cast<const float4*>(aux + c);
+        cv[j] = *reinterpret_cast<const float4*>(aux + 1024 + c);
+    }
+    uint32_t word[2] = {0u, 0u};   // scale bytes of bricks 0 / 1 (byte i & 3 = rows (i & 3)*16 + fr of the brick)
+    const int n = n0 + wn * 64 + fq * 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float2 st = *reinterpret_cast<const float2*>(aux + 2048 + (wm * 128 + i * 16 + fr) * 8);
+        const f32x2 rsx = {st.y, st.y}, rsy = {-st.y * st.x, -st.y * st.x};
+        uint32_t o[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f32x2 a01 = {acc[j][i][0], acc[j][i][1]}, a23 = {acc[j][i][2], acc[j][i][3]};
+            const f32x2 b01 = {bv[j].x, bv[j].y}, b23 = {bv[j].z, bv[j].w};
+            const f32x2 c01 = {cv[j].x, cv[j].y}, c23 = {cv[j].z, cv[j].w};
+            f32x2 v01 = __builtin_elementwise_fma(rsx, a01, __builtin_elementwise_fma(rsy, c01, b01));
+            f32x2 v23 = __builtin_elementwise_fma(rsx, a23, __builtin_elementwise_fma(rsy, c23, b23));
+            v01 = gelu_sig2(v01);
+            v23 = gelu_sig2(v23);
+            o[2 * j] = pack_bf2(v01.x, v01.y);
+            o[2 * j + 1] = pack_bf2(v23.x, v23.y);
+        }
+        const uint4 h0 = make_uint4(o[0], o[1], o[2], o[3]), h1 = make_uint4(o[4], o[5], o[6], o[7]);
+        uint32_t am = max(mx8_amax8(h0), mx8_amax8(h1));
+        const auto u = __builtin_amdgcn_permlane16_swap(am, am, false, false);   // partner fq ^ 1: the block's 32 columns
+        am = max((uint32_t)u[0], (uint32_t)u[1]);
+        const int E = mx8_block_exp(am);
+        word[i >> 2] |= (uint32_t)(E + 127) << (8 * (i & 3));
+        const uint2 q0 = mx8_pack8(h0, E), q1 = mx8_pack8(h1, E);
+        const int m = m0 + wm * 128 + i * 16 + fr;
+        if (m < M && n < N) *reinterpret_cast<uint4*>(o8.q + (int64_t)m * o8.ldq + n) = make_uint4(q0.x, q0.y, q1.x, q1.y);
+    }
+    // lanes fq and fq ^ 1 hold the same words (block fq >> 1): lane (fr, fq) stores brick fq & 1's
+    const int nb = n0 + wn * 64;
+    const int R = m0 + wm * 128 + (fq & 1) * 64;   // brick row base
+    if (nb < N && R < o8.lds)
+        reinterpret_cast<uint32_t*>(o8.s)[(int64_t)(nb >> 7) * o8.lds + R + (((nb >> 5) & 3) + (fq >> 1)) * 16 + fr] =
+            (fq & 1) ? word[1] : word[0];
+}
+
 // fp8-only output (no bf16 copy: FC1 -> FC2's A operand). Same image as store_wave_tile, read back 32 B per
 // lane (16 consecutive columns: 4 lanes per 64-column row, 8 iterations) so every element store is 16 B, and a
 // 32-column block is a lane pair (one DPP step). The wave owns whole scale words (its 128 rows are two 64-row

@@ -44,7 +44,8 @@ __device__ __forceinline__ void mx_col(f32x4 (&acc)[8], const i32x8& b, const i3
     VPF_MX(4, sa1); VPF_MX(5, sa1); VPF_MX(6, sa1); VPF_MX(7, sa1);
 }
 #undef VPF_MX
-template <int EPI, bool OUT8>
+// Q8D: fp8-only LN + GELU output (FC1) stored from the accumulators (store_wave_tile_q8_direct; W rows in wperm16 order)
+template <int EPI, bool OUT8, bool Q8D = false>
 __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict__ A, int lda,
                                                        const uint32_t* __restrict__ As, int lds_a,
                                                        const uint8_t* __restrict__ W,
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
         const int row = 8 * g + (lane >> 3);
         const int lch = (lane & 7) ^ ((row >> 1) & 7);
         offA[i] = (uint32_t)min(row, M - 1 - m0) * (uint32_t)lda + (uint32_t)(lch * 16);
-        offB[i] = (uint32_t)min(row, N - 1 - n0) * (uint32_t)K + (uint32_t)(lch * 16);
+        offB[i] = (uint32_t)min(Q8D ? wperm16(row) : row, N - 1 - n0) * (uint32_t)K + (uint32_t)(lch * 16);
     }
     // scale words: waves 0-3 DMA the A rows' 4 x 256 B, waves 4-7 the W rows' (4 B per lane, one piece per wave,
     // so every wave issues the same 9 pieces per K-tile and the counted waits below are wave-uniform); rows past
@@ -164,14 +165,32 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
             al[i] = lds16(la + row * 128 + (fq ^ sw) * 16);
             ah[i] = lds16(la + row * 128 + ((4 + fq) ^ sw) * 16);
         }
-        int sb = lds4(lbs + wn * 64 + fq * 16 + fr);
-        int sa0 = lds4(las + (2 * wm) * 64 + fq * 16 + fr);
-        int sa1 = lds4(las + (2 * wm + 1) * 64 + fq * 16 + fr);
-        // the reads have landed (the wait is tied to every fragment register so no use moves above it)
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(bl[0]), "+v"(bl[1]), "+v"(bl[2]), "+v"(bl[3]), "+v"(bh[0]), "+v"(bh[1]), "+v"(bh[2]),
-                       "+v"(bh[3]), "+v"(sb), "+v"(sa0), "+v"(sa1)
-                     :: "memory");
+        int sb, sa0, sa1;
+        if constexpr (Q8D) {
+            // LDS row j*16 + fr holds W row wperm16(j*16 + fr) = (fr >> 2)*16 + j*4 + (fr & 3) of the brick: its scale is
+            // byte fr >> 2 of word j*4 + (fr & 3); the four bytes are gathered into one word (byte j) by two v_perm_b32
+            const uint32_t* wb = lbs + wn * 64 + fq * 16 + (fr & 3);
+            int w0 = lds4(wb), w1 = lds4(wb + 4), w2 = lds4(wb + 8), w3 = lds4(wb + 12);
+            sa0 = lds4(las + (2 * wm) * 64 + fq * 16 + fr);
+            sa1 = lds4(las + (2 * wm + 1) * 64 + fq * 16 + fr);
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(bl[0]), "+v"(bl[1]), "+v"(bl[2]), "+v"(bl[3]), "+v"(bh[0]), "+v"(bh[1]), "+v"(bh[2]),
+                           "+v"(bh[3]), "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3), "+v"(sa0), "+v"(sa1)
+                         :: "memory");
+            const uint32_t f = (uint32_t)(fr >> 2);
+            const uint32_t lo = __builtin_amdgcn_perm((uint32_t)w1, (uint32_t)w0, 0x0c0c0000u | ((4u + f) << 8) | f);
+            const uint32_t hi = __builtin_amdgcn_perm((uint32_t)w3, (uint32_t)w2, ((4u + f) << 24) | (f << 16) | 0x0c0cu);
+            sb = (int)(lo | hi);
+        } else {
+            sb = lds4(lbs + wn * 64 + fq * 16 + fr);
+            sa0 = lds4(las + (2 * wm) * 64 + fq * 16 + fr);
+            sa1 = lds4(las + (2 * wm + 1) * 64 + fq * 16 + fr);
+            // the reads have landed (the wait is tied to every fragment register so no use moves above it)
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(bl[0]), "+v"(bl[1]), "+v"(bl[2]), "+v"(bl[3]), "+v"(bh[0]), "+v"(bh[1]), "+v"(bh[2]),
+                           "+v"(bh[3]), "+v"(sb), "+v"(sa0), "+v"(sa1)
+                         :: "memory");
+        }
         asm volatile(""
                      : "+v"(al[0]), "+v"(al[1]), "+v"(al[2]), "+v"(al[3]), "+v"(al[4]), "+v"(al[5]), "+v"(al[6]),
                        "+v"(al[7]), "+v"(ah[0]), "+v"(ah[1]), "+v"(ah[2]), "+v"(ah[3]), "+v"(ah[4]), "+v"(ah[5]),
@@ -219,6 +238,13 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_mx8(const uint8_t* __restrict
     // no LDS-DMA is outstanding after the K loop; saying so with the builtin (which hipcc's waitcnt pass reads,
     // unlike asm) keeps it from draining vmcnt(0) - and with it the residual loads - at the first LDS access below
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    if constexpr (Q8D) {   // no LDS image: only the LN combine above needs the barrier
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        store_wave_tile_q8_direct<EPI>(aux, acc, wm, wn, m0, n0, lane, M, N, o8);
+        return;
+    }
     uint4 res[16];
     if constexpr (EPI == VPF_EPI_BIAS_RESIDUAL) load_residual<false>(res, residual, wm, wn, m0, n0, lane, ldc, M, N);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // raw barrier: the residual loads stay in flight
@@ -261,7 +287,9 @@ __global__ __launch_bounds__(256) void k_quantize_mx8(const bf16_t* __restrict__
         C, (int)ldc, (int)M, (int)N, (int)K, group, stats_parts, ln_eps, stats_out, o8
 #define VPF_MX8_LAUNCH(E)                                                                                    \
     do {                                                                                                     \
-        if (o8.q)                                                                                            \
+        if (o8.q && !C && (E) == VPF_EPI_LN_GELU)                                                            \
+            hipLaunchKernelGGL((k_gemm_mx8<E, true, (E) == VPF_EPI_LN_GELU>), grid, block, 0, s, VPF_MX8_ARGS); \
+        else if (o8.q)                                                                                       \
             hipLaunchKernelGGL((k_gemm_mx8<E, true>), grid, block, 0, s, VPF_MX8_ARGS);                       \
         else                                                                                                 \
             hipLaunchKernelGGL((k_gemm_mx8<E, false>), grid, block, 0, s, VPF_MX8_ARGS);                      \
