@@ -160,7 +160,8 @@ def _run_multi(args, cfg, boxes, frames, MultiTracker, dist) -> int:
     for k, f in enumerate(frames, start=start):
         ests = mt.track(f)
         out.append({"frame": k, "targets": [{"x": x, "y": y, "scale": s} for x, y, s in ests]})
-        emit(k, f, [_box(st, b) for st, b in zip(ests, boxes)])
+        # the box sizes being tracked (restored from the checkpoint after --resume), not the config's
+        emit(k, f, [_box(st, (0.0, 0.0, w, h)) for st, (w, h) in zip(ests, mt.boxes)])
         if mt.rank == 0:
             print(f"frame {k:4d}  " + "  ".join(f"[{i}] x={x:8.2f} y={y:8.2f} s={s:6.3f}"
                                                  for i, (x, y, s) in enumerate(ests)), flush=True)

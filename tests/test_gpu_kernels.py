@@ -286,6 +286,42 @@ def test_gemm_kernel_variants_bit_identical(M, N, K, P):
         L.vpf_gemm_tune(0, -1)                # the per-shape defaults
 
 
+@pytest.mark.parametrize("epi", [1, 4, 5])
+@pytest.mark.parametrize("kern", [1, 5])
+def test_gemm_single_k_tile_epilogues_vs_fp64(epi, kern):
+    """K = 64 (one K-tile, nk = 1): the epilogue operands (bias, colsum, statistics planes) are DMA'd by some waves and
+    read by all, so they must land before the loop's only barrier (the deep-ring kernel issued them after
+    it, and its direct-store GELU epilogue could read stale bias). Bias + GELU, LN fold and LN fold + GELU on both
+    product kernels against float64, over 4096 tiles and three repeats with different bias values each time (a stale
+    read shows as a wrong column block)."""
+    from vitparticlefiltertracker_amd import _lib
+    L = _lib.lib()
+    M, N, K, P = 256 * 128, 8192, 64, 1
+    torch.manual_seed(epi * 10 + kern)
+    A = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    colsum = W.float().sum(1).contiguous()
+    st = torch.stack([torch.randn(M, device=DEV) * 0.1, torch.rand(M, device=DEV) + 0.5], 1).contiguous()
+    try:
+        assert L.vpf_gemm_tune(kern, -1) == 0
+        for rep in range(3):
+            bias = (torch.randn(N, device=DEV) * (rep + 1)).contiguous()
+            out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            if epi == 1:
+                vpf().gemm(A, W, bias, None, None, 0, None, None, 1, out)
+                ref = Fn.gelu(A.double() @ W.double().t() + bias.double())
+            else:
+                vpf().gemm(A, W, bias, None, None, 0, st, colsum, epi, out)
+                mean, rstd = st[:, 0].double(), st[:, 1].double()
+                ref = rstd[:, None] * (A.double() @ W.double().t()) - (rstd * mean)[:, None] * colsum.double() \
+                    + bias.double()
+                if epi == 5:
+                    ref = Fn.gelu(ref)
+            torch.testing.assert_close(out.double(), ref, rtol=1.6e-2, atol=2e-2)
+    finally:
+        L.vpf_gemm_tune(0, -1)
+
+
 def test_patch_and_cls_stats_planes():
     """EPI_PATCH + vpf_cls_rows_bf16 together fill the planes of every token row (patch rows by the GEMM, CLS
     rows by cls_rows), matching the stored bf16 token rows."""
@@ -828,7 +864,8 @@ def test_particle_filter_api_matches_oracle():
     """The ParticleFilter surface driven directly, 1000 particles over 5 frames: predict() equals the
     oracle's S2 walk bit for bit; update(features, template) gives Q = weights_to_Q of the kernel's cosine (itself
     within 1e-5 of numpy's); estimate() equals the oracle's S6 estimate; resample() returns the oracle's S7
-    ancestors and the particles become their states; `states` is the [P][3] view of the same storage."""
+    ancestors and the particles become their states; `particles` (and its alias `states`) is the [P][3] view of the SoA
+    storage `particles_soa`."""
     from vitparticlefiltertracker_amd.particle_filter import ParticleFilter
     P, D, seed = 1000, 192, 321
     std, srange = (3.0, 2.0, 0.03), (0.6, 1.8)
@@ -841,8 +878,12 @@ def test_particle_filter_api_matches_oracle():
     for k in range(1, 6):
         f.predict()
         pf.predict(ref, 0, seed, k, std, 224, 224, srange)
-        assert np.array_equal(f.particles.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"frame {k}: predict"
+        assert np.array_equal(f.particles_soa.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"frame {k}: predict"
         assert f.states.shape == (P, 3) and torch.equal(f.states.cpu(), torch.from_numpy(ref.T.copy()))
+        # a §8b-style caller: particles is [P, 3], so column 0 is every particle's x
+        assert f.particles.shape == (P, 3)
+        for c in range(3):
+            assert np.array_equal(f.particles[:, c].cpu().numpy().view(np.uint32), ref[c].view(np.uint32))
         feat = (rng.standard_normal((P, D)) + 2.0 * t).astype(np.float32)
         Q = f.update(torch.from_numpy(feat).to(DEV), torch.from_numpy(t).to(DEV)).cpu().numpy()
         sim = torch.empty(P, device=DEV)
@@ -858,4 +899,4 @@ def test_particle_filter_api_matches_oracle():
         anc_ref = pf.resample(Q, pf.resample_U(seed, k))
         assert np.array_equal(anc, anc_ref), f"frame {k}: ancestors"
         ref = np.ascontiguousarray(ref[:, anc_ref])
-        assert np.array_equal(f.particles.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"frame {k}: states"
+        assert np.array_equal(f.particles_soa.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"frame {k}: states"

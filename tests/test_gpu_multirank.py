@@ -35,7 +35,7 @@ def _run(tr, clip):
     tr.init(clip[0], (80, 80, 64, 64))
     for f in clip[1:]:
         est = tr.track(f)
-        out.append((est, tr.pf.last_ancestors.cpu().numpy().copy(), tr.pf.particles.cpu().numpy().copy()))
+        out.append((est, tr.pf.last_ancestors.cpu().numpy().copy(), tr.pf.particles_soa.cpu().numpy().copy()))
     return out
 
 
@@ -112,7 +112,7 @@ def _mt_run(mt, clip):
         Qs = [pf.Q.cpu().numpy().copy() for pf in mt.pfs]
         ests = mt.step()
         out.append((ests, [pf.last_ancestors.cpu().numpy().copy() for pf in mt.pfs],
-                    [pf.particles.cpu().numpy().copy() for pf in mt.pfs], Qs))
+                    [pf.particles_soa.cpu().numpy().copy() for pf in mt.pfs], Qs))
     return out
 
 

@@ -81,7 +81,7 @@ def _check_frames(arch_name: str, P: int, frames: int, n_sample: int, dtype: str
         tr.pf.predict(tr.frame_index)
         tr.weigh()                                          # HIP-graph replay: crop + ViT + weights
         Q = tr.pf.Q.cpu().numpy().copy()
-        pred = tr.pf.particles.cpu().numpy().copy()
+        pred = tr.pf.particles_soa.cpu().numpy().copy()
         # LN'd CLS features and similarities of this forward's tokens (recomputed eagerly: same Q bits)
         tr.engine.weights_from_tokens(tr.n_local, tr.template, tr.lam, tr.bits, want_feat=True)
         assert np.array_equal(tr.engine.Q[:P].cpu().numpy(), Q)
@@ -104,7 +104,7 @@ def _check_frames(arch_name: str, P: int, frames: int, n_sample: int, dtype: str
         e_ref = ot.track(f, Q=Q)
         np.testing.assert_allclose(e_gpu, e_ref, rtol=1e-12)
         assert np.array_equal(anc, ot.last_ancestors), f"frame {k}: ancestors"
-        assert np.array_equal(tr.pf.particles.cpu().numpy().view(np.uint32), ot.particles.view(np.uint32))
+        assert np.array_equal(tr.pf.particles_soa.cpu().numpy().view(np.uint32), ot.particles.view(np.uint32))
         assert Q.sum() > 0
     return tr
 
@@ -168,12 +168,12 @@ def _c2_run(tr, clip, bbox=BBOX0, sample=None):
         Q = tr.pf.Q.cpu().numpy().copy()
         extra = None
         if sample is not None:
-            pred = tr.pf.particles.cpu().numpy()[:, sample].copy()
+            pred = tr.pf.particles_soa.cpu().numpy()[:, sample].copy()
             tr.engine.weights_from_tokens(tr.n_local, tr.template, tr.lam, tr.bits, want_feat=True)
             assert np.array_equal(tr.engine.Q[:tr.n_local].cpu().numpy(), Q)
             extra = (pred, tr.engine.feat[:tr.n_local][torch.from_numpy(sample).to(tr.device)].double().cpu())
         est = tr.pf.step()
-        out.append((est, Q, tr.pf.last_ancestors.cpu().numpy().copy(), tr.pf.particles.cpu().numpy().copy(), extra))
+        out.append((est, Q, tr.pf.last_ancestors.cpu().numpy().copy(), tr.pf.particles_soa.cpu().numpy().copy(), extra))
     return out
 
 

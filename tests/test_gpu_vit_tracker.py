@@ -139,9 +139,47 @@ def test_tracker_bf16_weight_injection_bit_exact(use_graph, dtype, arch_name, P)
         anc = tr.pf.resample().cpu().numpy()
         e_ref = ot.track(f, Q=Q)                      # oracle predicts itself, then uses the GPU's weights
         assert np.array_equal(anc, ot.last_ancestors), f"frame {k}"
-        assert np.array_equal(tr.pf.particles.cpu().numpy().view(np.uint32), ot.particles.view(np.uint32))
+        assert np.array_equal(tr.pf.particles_soa.cpu().numpy().view(np.uint32), ot.particles.view(np.uint32))
         np.testing.assert_allclose(e_gpu, e_ref, rtol=1e-12)
         assert Q.sum() > 0
+
+
+def test_configs0_32_frame_clip_matches_oracle():
+    """BASELINE.json configs[0] as written: 256 particles, ViT-Ti/16, a 32-frame synthetic 224 x 224
+    clip, run by the GPU Tracker (bf16, HIP-graph replay, the product's step(): estimate and resample in one device
+    call) against OracleTracker with the GPU's int64 weights injected every frame. All 31 tracked frames: every
+    ancestor and particle state bit-exact, the estimate within 1e-12 relative. Every 8th frame the bf16 CLS features of
+    4 predicted particles are also checked against the fp32 oracle's (cosine >= 0.999)."""
+    from vitparticlefiltertracker_amd import Tracker
+    cfg = _tiny_cfg(256, "bf16")
+    arch = ARCHS["vit_tiny_patch16_224"]
+    w = make_vit_weights(arch, seed=3)
+    clip = synthetic_clip(32)
+    assert len(clip) == 32 and clip[0].shape == (224, 224, 3)
+    tr = Tracker(cfg, weights=w)
+    ot = OracleTracker(cfg, w, arch)
+    tr.init(clip[0], (80, 80, 64, 64))
+    ot.init(clip[0], (80, 80, 64, 64))
+    for k, f in enumerate(clip[1:], start=1):
+        tr._upload(f)
+        tr.frame_index += 1
+        tr.pf.predict(tr.frame_index)
+        tr.weigh()
+        Q = tr.pf.Q.cpu().numpy().copy()
+        assert Q.sum() > 0, f"frame {k}"
+        if k % 8 == 0:
+            pred = tr.pf.particles_soa.cpu().numpy()
+            tr.engine.weights_from_tokens(tr.n_local, tr.template, tr.lam, tr.bits, want_feat=True)
+            idx = np.array([0, 85, 170, 255])
+            feat = tr.engine.feat[idx.tolist()].double().cpu().numpy()
+            ref_f = ot.features(f, np.ascontiguousarray(pred[:, idx])).astype(np.float64)
+            cos = (feat * ref_f).sum(1) / (np.linalg.norm(feat, axis=1) * np.linalg.norm(ref_f, axis=1))
+            assert cos.min() >= 0.999, (k, cos)
+        e_gpu = tr.pf.step()
+        e_ref = ot.track(f, Q=Q)
+        assert np.array_equal(tr.pf.last_ancestors.cpu().numpy(), ot.last_ancestors), f"frame {k}: ancestors"
+        assert np.array_equal(tr.pf.particles_soa.cpu().numpy().view(np.uint32), ot.particles.view(np.uint32)), k
+        np.testing.assert_allclose(e_gpu, e_ref, rtol=1e-12)
 
 
 @pytest.mark.parametrize("dtype,arch_name", [("bf16", "vit_tiny_patch16_224"), ("fp8", "vit_small_patch16_224")])
@@ -328,7 +366,7 @@ def test_multitracker_one_target_equals_tracker():
         a = tr.track(f)
         (b,) = mt.track(f)
         assert a == b
-    assert torch.equal(tr.pf.particles, mt.pfs[0].particles)
+    assert torch.equal(tr.pf.particles_soa, mt.pfs[0].particles_soa)
 
 
 TWO_BOXES = [(40, 50, 48, 48), (200, 150, 64, 40)]
@@ -418,7 +456,7 @@ def test_tracker_template_update_bf16_q_injected():
         e_ref = ot.track(f, Q=Q)                       # oracle: predict, injected Q, estimate, resample, S9 update
         np.testing.assert_allclose(est, e_ref, rtol=1e-12)
         assert np.array_equal(tr.pf.last_ancestors.cpu().numpy(), ot.last_ancestors), f"frame {k}"
-        assert np.array_equal(tr.pf.particles.cpu().numpy().view(np.uint32), ot.particles.view(np.uint32))
+        assert np.array_equal(tr.pf.particles_soa.cpu().numpy().view(np.uint32), ot.particles.view(np.uint32))
         cos = float(np.dot(tr.template.cpu().numpy().astype(np.float64), ot.template.astype(np.float64)))
         assert cos > 0.999, (k, cos)
 
@@ -476,7 +514,7 @@ def test_multitracker_bf16_q_injected(alpha):
         for k in range(2):
             np.testing.assert_allclose(e_gpu[k], e_ref[k], rtol=1e-12)
             assert np.array_equal(mt.pfs[k].last_ancestors.cpu().numpy(), om.targets[k].last_ancestors), (t, k)
-            assert np.array_equal(mt.pfs[k].particles.cpu().numpy().view(np.uint32),
+            assert np.array_equal(mt.pfs[k].particles_soa.cpu().numpy().view(np.uint32),
                                   om.targets[k].particles.view(np.uint32)), (t, k)
             cos = float(np.dot(mt.templates[k].cpu().numpy().astype(np.float64),
                                om.targets[k].template.astype(np.float64)))
@@ -507,7 +545,7 @@ def test_tracker_upload_mixed_sources_and_size_change():
     small = np.ascontiguousarray(clip[5][:100, :120])
     tr.track(small)
     assert (tr.pf.height, tr.pf.width) == (100, 120)
-    p = tr.pf.particles.cpu().numpy()
+    p = tr.pf.particles_soa.cpu().numpy()
     assert p[0].max() <= 119 and p[1].max() <= 99 and p.min() >= 0
 
 
@@ -524,7 +562,7 @@ def test_checkpoint_resume_bit_exact(tmp_path, alpha):
     clip = synthetic_clip(7)
 
     def run(tr, frames):
-        return [(tr.track(f), tr.pf.last_ancestors.cpu().numpy().copy(), tr.pf.particles.cpu().numpy().copy())
+        return [(tr.track(f), tr.pf.last_ancestors.cpu().numpy().copy(), tr.pf.particles_soa.cpu().numpy().copy())
                 for f in frames]
 
     tr = Tracker(cfg, weights=w)

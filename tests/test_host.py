@@ -225,6 +225,24 @@ def test_weights_digest_tracks_the_weight_set():
     assert weights_digest(w) != d0
 
 
+def test_checkpoint_formats_are_refused_with_a_reason():
+    """the weights' crc32 joined the fingerprint in round 4, so the format is now 3; format 1 and format 2
+    files get an explicit 're-create the checkpoint' message instead of a generic configuration mismatch."""
+    import json
+    from vitparticlefiltertracker_amd.tracker import CHECKPOINT_FORMAT, _check_fingerprint
+    assert CHECKPOINT_FORMAT == 3
+    mine = {"arch": "vit_tiny_patch16_224", "weights_crc32": "0123abcd", "P": 16}
+    cfg = np.array(json.dumps(mine))
+    _check_fingerprint({"format": np.int64(3), "config": cfg}, mine)
+    for fmt, words in ((1, "format 1"), (2, "crc32")):
+        with pytest.raises(ValueError, match=words):
+            _check_fingerprint({"format": np.int64(fmt), "config": cfg}, mine)
+    with pytest.raises(ValueError, match="weights_crc32"):
+        _check_fingerprint({"format": np.int64(3), "config": cfg}, {**mine, "weights_crc32": "ffffffff"})
+    with pytest.raises(ValueError, match="unknown"):
+        _check_fingerprint({"format": np.int64(9), "config": cfg}, mine)
+
+
 def _vregs(tok):
     m = re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
     if m:

@@ -37,7 +37,7 @@ def main():
         ref.set_weights(Q)
         e1, e0 = pfs.step(), ref.step()
         same = (e1 == e0 and torch.equal(pfs.last_ancestors, ref.last_ancestors[rank * pfs.n_local:(rank + 1) * pfs.n_local])
-                and torch.equal(pfs.particles, ref.particles[:, rank * pfs.n_local:(rank + 1) * pfs.n_local]))
+                and torch.equal(pfs.particles_soa, ref.particles_soa[:, rank * pfs.n_local:(rank + 1) * pfs.n_local]))
         ok &= same
         print(f"rank {rank} frame {k}: estimate {e1} single-rank {e0} bit-exact {same}", flush=True)
     dist.destroy_process_group()

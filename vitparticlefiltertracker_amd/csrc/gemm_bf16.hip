@@ -157,6 +157,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
     stage_a(0);
     stage_b(0);
     if (nk > 1) stage_a(1);
+    // The epilogue operands must land before a barrier that every wave passes ahead of the epilogue: one wave DMAs the
+    // bias, others the colsum and the planes, and every wave reads all of them. At nk >= 2 they are issued at K-tile
+    // nk - 2 and the last K-step's vmcnt(0) + barrier retires them; at nk == 1 (K = 64) that barrier is the loop's only
+    // one, so they go out with the prologue (issued after it, the direct-store GELU epilogue read bias that
+    // waves 0 / 1 had not yet landed).
+    if (nk == 1) load_aux();
     for (int kt = 0; kt < nk; ++kt) {
         // issue order: A0 B0 A1 | per K-tile t: B(t+1) A(t+2). A(kt), B(kt) are older than everything but A(kt+1)
         // (4 pieces per wave) until the last two K-tiles, where the tail is B / aux only.
@@ -164,7 +170,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gemm_bf16(const bf16_t* __restrict
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (kt == (nk >= 2 ? nk - 2 : 0)) load_aux();
+        if (nk >= 2 && kt == nk - 2) load_aux();
         if (wide && kt == nk - 1) load_planes(planes_lds);   // slot of A(nk-2): free after this barrier
         const char* la = smem + (kt % 3) * OPERAND_BYTES;
         const char* lb = smem + (3 + (kt & 1)) * OPERAND_BYTES;

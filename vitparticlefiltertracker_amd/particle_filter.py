@@ -149,9 +149,10 @@ def compact_view(glob: torch.Tensor, P: int):
 
 class ParticleFilter:
     """H1, H10-H12. API: predict(), update(features, template), estimate(), resample(),
-    attributes `particles` (float32[3][P_local] on the device, SoA rows x, y, scale) and `Q` (int64[P_local]).
+    attributes `particles` (float32[P_local][3] on the device: one (x, y, scale) row per particle, §8b's shape) and
+    `Q` (int64[P_local]). The storage is SoA, `particles_soa` (float32[3][P_local]); `particles` is its transposed view.
 
-    Both attributes are views into one shard chunk (`shard_views`). Per frame (`step`, or estimate() then
+    `Q` and `particles_soa` are views into one shard chunk (`shard_views`). Per frame (`step`, or estimate() then
     resample()): world > 1 all-gathers the chunks (20 B per particle, one fixed-size RCCL collective), then ONE
     device call, vpf_estimate_resample, computes the estimate sums, the CDF, the resample word and the ancestors
     of this rank's slots over the global set. The resample is enqueued before the host waits for the 32-B
@@ -177,7 +178,7 @@ class ParticleFilter:
         self.height, self.width = int(frame_size[0]), int(frame_size[1])
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self._chunk = torch.zeros(chunk_words(n_max), device=self.device, dtype=torch.int32)
-        self.Q, self.particles = shard_views(self._chunk, n)
+        self.Q, self.particles_soa = shard_views(self._chunk, n)
         self._cidx = None
         if self.world_size > 1:
             self._allc = torch.zeros(self.world_size * chunk_words(n_max), device=self.device, dtype=torch.int32)
@@ -188,7 +189,7 @@ class ParticleFilter:
                 self._glob = torch.empty(5 * self.P, device=self.device, dtype=torch.int32)
                 self._gview = compact_view(self._glob, self.P)
         else:
-            self._gview = (self.Q, n, self.particles.view(-1), n, 3 * n, n)
+            self._gview = (self.Q, n, self.particles_soa.view(-1), n, 3 * n, n)
         self._cdf = torch.empty(self.P, device=self.device, dtype=torch.int64)
         self._states = torch.empty(3, n, device=self.device, dtype=torch.float32)
         self._anc = torch.empty(n, device=self.device, dtype=torch.int32)
@@ -203,16 +204,31 @@ class ParticleFilter:
 
     # ------------------------------------------------------------------ state
     @property
+    def particles(self) -> torch.Tensor:
+        """The particles as float32[P_local][3] rows (x, y, scale): SURVEY.md §8b's `.particles [P, 3]`, so
+        `particles[:, 0]` is every particle's x. A transposed VIEW of the SoA storage `particles_soa` (float32[3][P_local],
+        the layout the kernels and the all-gathered chunk use); writes through it land in the filter's state."""
+        return self.particles_soa.t()
+
+    @particles.setter
+    def particles(self, value) -> None:
+        """Assign [P_local][3] states (x, y, scale per row): copied into the SoA storage."""
+        v = torch.as_tensor(value, dtype=torch.float32, device=self.device)
+        if tuple(v.shape) != (self.n_local, 3):
+            raise ValueError(f"particles: expected shape ({self.n_local}, 3), got {tuple(v.shape)}")
+        self.particles_soa.copy_(v.t())
+        self._settled = False
+
+    @property
     def states(self) -> torch.Tensor:
-        """The particles as float32[P_local][3] rows (x, y, scale): a transposed VIEW of the SoA `particles`
-        (SURVEY.md §8b's [P, 3] shape); writes through it land in the filter's state."""
-        return self.particles.t()
+        """Alias of `particles` ([P_local][3] view)."""
+        return self.particles_soa.t()
 
     def reset(self, state) -> None:
         x, y, s = (float(v) for v in state)
-        self.particles[0].fill_(x)
-        self.particles[1].fill_(y)
-        self.particles[2].fill_(s)
+        self.particles_soa[0].fill_(x)
+        self.particles_soa[1].fill_(y)
+        self.particles_soa[2].fill_(s)
         self.Q.zero_()
         self.frame = 0
         self._settled = False
@@ -220,7 +236,7 @@ class ParticleFilter:
     def predict(self, frame: Optional[int] = None) -> None:
         """H1: counter-based random walk (SPEC S2) for frame index `frame` (default: next frame)."""
         self.frame = self.frame + 1 if frame is None else int(frame)
-        vpf.predict_(self.particles, self.begin, self.seed, self.frame, self.motion_std, float(self.width),
+        vpf.predict_(self.particles_soa, self.begin, self.seed, self.frame, self.motion_std, float(self.width),
                      float(self.height), self.scale_range)
         self._settled = False
 
@@ -259,7 +275,7 @@ class ParticleFilter:
 
     def _commit(self) -> None:
         """Enqueue the resample computed by _settle: this rank's slots take their ancestors' states."""
-        self.particles.copy_(self._states)
+        self.particles_soa.copy_(self._states)
         self.last_ancestors = self._anc.clone()
         self.Q.zero_()
         self._settled = False

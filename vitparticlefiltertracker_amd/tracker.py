@@ -39,6 +39,70 @@ def weights_digest(weights) -> str:
     return f"{crc:08x}"
 
 
+# 3: the fingerprint includes the weights' crc32 (round 4 added it to format 2 without a bump: ADVICE r4)
+CHECKPOINT_FORMAT = 3
+
+
+def _stage_frame(self, frame) -> torch.Tensor:
+    """Frame -> the device frame buffer `self._frame_dev` (Tracker and MultiTracker): a device tensor is copied on the
+    device; a pinned uint8[H][W][3] tensor (frames.prefetch) is copied asynchronously; anything else goes through a
+    pinned staging buffer `self._frame_host` and an asynchronous copy guarded by the event `self._h2d_done`, so the host
+    never blocks on the H2D copy of the frame it just submitted. A new frame shape drops the captured graph."""
+    if isinstance(frame, torch.Tensor) and frame.is_cuda:
+        src = frame.to(torch.uint8)
+        if self._frame_dev is None or self._frame_dev.shape != src.shape:
+            self._frame_dev = torch.empty_like(src)
+            self._graph = None
+        self._frame_dev.copy_(src)
+        return self._frame_dev
+    if (isinstance(frame, torch.Tensor) and frame.dtype == torch.uint8 and frame.dim() == 3
+            and frame.shape[2] == 3 and frame.is_contiguous() and frame.is_pinned()):
+        # frames.prefetch() output: already staged in pinned memory, copy straight from it
+        if self._frame_dev is None or self._frame_dev.shape != frame.shape:
+            self._frame_dev = torch.empty(frame.shape, dtype=torch.uint8, device=self.device)
+            self._graph = None
+        self._frame_dev.copy_(frame, non_blocking=True)
+        return self._frame_dev
+    arr = np.ascontiguousarray(frame.cpu().numpy() if isinstance(frame, torch.Tensor) else frame, dtype=np.uint8)
+    if arr.ndim != 3 or arr.shape[2] != 3:
+        raise ValueError("frame must be uint8[H][W][3]")
+    if self._frame_dev is None or tuple(self._frame_dev.shape) != arr.shape:
+        self._frame_dev = torch.empty(arr.shape, dtype=torch.uint8, device=self.device)
+        self._graph = None
+    # the pinned staging buffer is sized independently: the device frame may have come from a pinned or
+    # device tensor of this shape, which never touches it
+    if self._frame_host is None or tuple(self._frame_host.shape) != arr.shape:
+        # the previous async copy may still read the old buffer: finish it before dropping it
+        if self._frame_host is not None:
+            torch.cuda.current_stream(self.device).synchronize()
+        self._frame_host = torch.empty(arr.shape, dtype=torch.uint8).pin_memory()
+    elif self._h2d_done is not None:
+        # reusing the staging buffer: the last frame's H2D copy must have finished reading it
+        self._h2d_done.synchronize()
+    self._frame_host.numpy()[...] = arr
+    self._frame_dev.copy_(self._frame_host, non_blocking=True)
+    if self._h2d_done is None:
+        self._h2d_done = torch.cuda.Event()
+    self._h2d_done.record()
+    return self._frame_dev
+
+
+class _LazyDigest:
+    """`weights_digest` of the tracker's weights, computed on first use (a checkpoint save / load) and cached: the crc32
+    converts every weight to a host fp32 copy (~1.2 GB for ViT-L/14), which a tracker that never checkpoints should not
+    pay at construction. Weights built from the seed are rebuilt from it (make_vit_weights is
+    deterministic); weights passed in are the caller's tensors, referenced, not copied."""
+
+    @property
+    def weights_digest(self) -> str:
+        if self._digest is None:
+            w = self._weights_arg
+            if w is None:
+                w = make_vit_weights(self.arch, seed=int(self.cfg["model"]["weights"]["seed"]))
+            self._digest = weights_digest(w)
+        return self._digest
+
+
 def _fingerprint(cfg, arch_name: str, digest: str, rank: int, world_size: int) -> dict:
     """Every configuration value a tracking frame's arithmetic depends on: a checkpoint records these and
     a resume under any other value is refused instead of drifting from the original run."""
@@ -56,10 +120,14 @@ def _check_fingerprint(sd: dict, mine: dict) -> None:
     import json
     fmt = int(sd["format"])
     if fmt == 1:
-        raise ValueError("checkpoint format 1 (rounds 1-2) records only P, rank, world size, seed and arch; format 2 "
-                         "also checks every value the tracking arithmetic depends on (dtype, lambda, motion, "
-                         "weights, ...): re-create the checkpoint with this version")
-    if fmt != 2:
+        raise ValueError("checkpoint format 1 (rounds 1-2) records only P, rank, world size, seed and arch; format "
+                         f"{CHECKPOINT_FORMAT} also checks every value the tracking arithmetic depends on (dtype, lambda, "
+                         "motion, weights, ...): re-create the checkpoint with this version")
+    if fmt == 2:
+        raise ValueError("checkpoint format 2 (round 4) does not record the weights' crc32, which format "
+                         f"{CHECKPOINT_FORMAT} checks so that a resume with other weights is refused: re-create the "
+                         "checkpoint with this version")
+    if fmt != CHECKPOINT_FORMAT:
         raise ValueError(f"unknown checkpoint format {fmt}")
     saved = json.loads(str(sd["config"]))
     diff = sorted(k for k in set(saved) | set(mine) if saved.get(k) != mine.get(k))
@@ -90,7 +158,7 @@ def _dist_info(rank, world_size, group):
     return 0, 1, None
 
 
-class Tracker:
+class Tracker(_LazyDigest):
     def __init__(self, cfg=None, device=None, rank: Optional[int] = None, world_size: Optional[int] = None,
                  group=None, use_graph: bool = True, weights=None):
         self.cfg = load_config(cfg)
@@ -107,7 +175,7 @@ class Tracker:
         P = int(c["particles"]["num"])
         _, self.n_local = shard_range(P, self.world_size, self.rank)   # rank r: [floor(rP/G), floor((r+1)P/G))
         w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
-        self.weights_digest = weights_digest(w)
+        self._weights_arg, self._digest = weights, None
         self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, max(1, self.n_local),
                                 c["model"]["mean"], c["model"]["std"])
         self.lam = float(c["likelihood"]["lambda"])
@@ -125,43 +193,7 @@ class Tracker:
 
     # ------------------------------------------------------------------ frames
     def _upload(self, frame) -> torch.Tensor:
-        if isinstance(frame, torch.Tensor) and frame.is_cuda:
-            src = frame.to(torch.uint8)
-            if self._frame_dev is None or self._frame_dev.shape != src.shape:
-                self._frame_dev = torch.empty_like(src)
-                self._graph = None
-            self._frame_dev.copy_(src)
-            return self._frame_dev
-        if (isinstance(frame, torch.Tensor) and frame.dtype == torch.uint8 and frame.dim() == 3
-                and frame.shape[2] == 3 and frame.is_contiguous() and frame.is_pinned()):
-            # frames.prefetch() output: already staged in pinned memory, copy straight from it
-            if self._frame_dev is None or self._frame_dev.shape != frame.shape:
-                self._frame_dev = torch.empty(frame.shape, dtype=torch.uint8, device=self.device)
-                self._graph = None
-            self._frame_dev.copy_(frame, non_blocking=True)
-            return self._frame_dev
-        arr = np.ascontiguousarray(frame.cpu().numpy() if isinstance(frame, torch.Tensor) else frame, dtype=np.uint8)
-        if arr.ndim != 3 or arr.shape[2] != 3:
-            raise ValueError("frame must be uint8[H][W][3]")
-        if self._frame_dev is None or tuple(self._frame_dev.shape) != arr.shape:
-            self._frame_dev = torch.empty(arr.shape, dtype=torch.uint8, device=self.device)
-            self._graph = None
-        # the pinned staging buffer is sized independently: the device frame may have come from a pinned or
-        # device tensor of this shape, which never touches it
-        if self._frame_host is None or tuple(self._frame_host.shape) != arr.shape:
-            # the previous async copy may still read the old buffer: finish it before dropping it
-            if self._frame_host is not None:
-                torch.cuda.current_stream(self.device).synchronize()
-            self._frame_host = torch.empty(arr.shape, dtype=torch.uint8).pin_memory()
-        elif self._h2d_done is not None:
-            # reusing the staging buffer: the last frame's H2D copy must have finished reading it
-            self._h2d_done.synchronize()
-        self._frame_host.numpy()[...] = arr
-        self._frame_dev.copy_(self._frame_host, non_blocking=True)
-        if self._h2d_done is None:
-            self._h2d_done = torch.cuda.Event()
-        self._h2d_done.record()
-        return self._frame_dev
+        return _stage_frame(self, frame)
 
     # ------------------------------------------------------------------ H13
     def init(self, frame, bbox) -> None:
@@ -187,7 +219,7 @@ class Tracker:
 
     # ------------------------------------------------------------------ H14
     def _features_to_weights(self) -> None:
-        self.engine.forward_weights(self._frame_dev, self.pf.particles, self.box_wh, self.template, self.lam,
+        self.engine.forward_weights(self._frame_dev, self.pf.particles_soa, self.box_wh, self.template, self.lam,
                                     self.bits)
 
     def _capture(self) -> None:
@@ -254,8 +286,8 @@ class Tracker:
         import json
         if self.pf is None:
             raise RuntimeError("call init(frame, bbox) first")
-        return {"format": np.int64(2), "frame_index": np.int64(self.frame_index),
-                "pf_frame": np.int64(self.pf.frame), "particles": self.pf.particles.cpu().numpy(),
+        return {"format": np.int64(CHECKPOINT_FORMAT), "frame_index": np.int64(self.frame_index),
+                "pf_frame": np.int64(self.pf.frame), "particles": self.pf.particles_soa.cpu().numpy(),
                 "template": self.template.cpu().numpy(), "box_wh": np.array(self.box_wh, np.float64),
                 "frame_hw": np.array([self.pf.height, self.pf.width], np.int64),
                 "config": np.array(json.dumps(self.config_fingerprint(), sort_keys=True))}
@@ -278,7 +310,7 @@ class Tracker:
                                      self.lam, self.bits, self.rank, self.world_size, self.group)
         self.pf.reset((0.0, 0.0, 1.0))
         self.pf.height, self.pf.width = H, W
-        self.pf.particles.copy_(torch.from_numpy(np.ascontiguousarray(sd["particles"], dtype=np.float32)))
+        self.pf.particles_soa.copy_(torch.from_numpy(np.ascontiguousarray(sd["particles"], dtype=np.float32)))
         self.pf.frame = int(sd["pf_frame"])
         self.frame_index = int(sd["frame_index"])
         self._graph = None
@@ -308,7 +340,7 @@ class Tracker:
         return np.array([self.track(f) for f in frames], dtype=np.float64)
 
 
-class MultiTracker:
+class MultiTracker(_LazyDigest):
     """Several targets in one frame loop (SPEC S9): one ParticleFilter per target, and ONE
     batched ViT forward over every target's particles per frame (crops with each target's own template box, one patch
     GEMM / encoder / final LN over all K*P crops, cosine weights against each target's own template), captured
@@ -338,7 +370,7 @@ class MultiTracker:
         self.P = int(c["particles"]["num"])
         _, self.n_local = shard_range(self.P, self.world_size, self.rank)
         w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
-        self.weights_digest = weights_digest(w)
+        self._weights_arg, self._digest = weights, None
         self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, self.K * self.n_local,
                                 c["model"]["mean"], c["model"]["std"])
         self.lam = float(c["likelihood"]["lambda"])
@@ -349,17 +381,13 @@ class MultiTracker:
         self.templates: List[torch.Tensor] = []
         self.boxes: List[Tuple[float, float]] = []
         self._frame_dev: Optional[torch.Tensor] = None
+        self._frame_host: Optional[torch.Tensor] = None
+        self._h2d_done: Optional[torch.cuda.Event] = None
         self._graph = None
         self.frame_index = 0
 
     def _upload(self, frame) -> torch.Tensor:
-        arr = torch.as_tensor(np.ascontiguousarray(frame.cpu().numpy() if isinstance(frame, torch.Tensor) else frame,
-                                                   dtype=np.uint8))
-        if self._frame_dev is None or tuple(self._frame_dev.shape) != tuple(arr.shape):
-            self._frame_dev = torch.empty(arr.shape, dtype=torch.uint8, device=self.device)
-            self._graph = None
-        self._frame_dev.copy_(arr)
-        return self._frame_dev
+        return _stage_frame(self, frame)   # pinned staging + async copy, as Tracker
 
     def init(self, frame, bboxes: Sequence) -> None:
         if len(bboxes) != self.K:
@@ -383,7 +411,7 @@ class MultiTracker:
 
     def _forward(self) -> None:
         eng = self.engine
-        n = eng.embed_many(self._frame_dev, [pf.particles for pf in self.pfs], self.boxes)
+        n = eng.embed_many(self._frame_dev, [pf.particles_soa for pf in self.pfs], self.boxes)
         eng.encoder(n)
         for k in range(self.K):
             eng.weights_from_tokens(self.n_local, self.templates[k], self.lam, self.bits, row0=k * self.n_local)
@@ -443,9 +471,9 @@ class MultiTracker:
         import json
         if not self.pfs:
             raise RuntimeError("call init(frame, bboxes) first")
-        return {"format": np.int64(2), "n_objects": np.int64(self.K), "frame_index": np.int64(self.frame_index),
+        return {"format": np.int64(CHECKPOINT_FORMAT), "n_objects": np.int64(self.K), "frame_index": np.int64(self.frame_index),
                 "pf_frame": np.array([pf.frame for pf in self.pfs], np.int64),
-                "particles": np.stack([pf.particles.cpu().numpy() for pf in self.pfs]),
+                "particles": np.stack([pf.particles_soa.cpu().numpy() for pf in self.pfs]),
                 "template": np.stack([t.cpu().numpy() for t in self.templates]),
                 "box_wh": np.array(self.boxes, np.float64),
                 "frame_hw": np.array([self.pfs[0].height, self.pfs[0].width], np.int64),
@@ -469,7 +497,7 @@ class MultiTracker:
         for k, pf in enumerate(self.pfs):
             pf.reset((0.0, 0.0, 1.0))
             pf.height, pf.width = H, W
-            pf.particles.copy_(torch.from_numpy(np.ascontiguousarray(sd["particles"][k], dtype=np.float32)))
+            pf.particles_soa.copy_(torch.from_numpy(np.ascontiguousarray(sd["particles"][k], dtype=np.float32)))
             pf.frame = int(sd["pf_frame"][k])
             # in place: a captured graph reads these buffers
             self.templates[k].copy_(torch.from_numpy(np.ascontiguousarray(sd["template"][k], dtype=np.float32)))
