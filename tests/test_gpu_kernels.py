@@ -559,11 +559,14 @@ def _attn_ref64(qkv, H):
 
 
 @pytest.mark.parametrize("B,N,H", [(100, 197, 12), (90, 256, 12), (96, 280, 12), (80, 111, 12), (70, 33, 6),
-                                   (4096, 197, 12)])
+                                   (4096, 197, 12), (64, 577, 16), (40, 400, 8), (30, 640, 16), (50, 300, 12)])
 def test_attention_bf16_large(B, N, H):
     """B*H >= 4 x CUs; (4096, 197, 12) is the configs[1] launch. N <= 256 runs the key-pipelined kernel (with the
-    16-query tail strip when the last strip holds <= 16 real queries: N = 197 / 111 / 33), N = 280 the whole-image
-    kernel (9 query strips: a wave also takes a second strip). Against an fp64 reference on at most 512 particles:
+    16-query tail strip when the last strip holds <= 16 real queries: N = 197 / 111 / 33). N > 256 runs the key-streamed
+    kernel (round 5): 6-strip query blocks, K / V through a 9-chunk ring. N = 577 (configs[3], 64 x 16 units): 3 blocks
+    and the 16-query strip of query 576 on wave 0 of the last block beside its 32-query strip; N = 400: the same with
+    16 tail queries; N = 300: the 16-query strip on a wave of its own; N = 280: a partial 32-query strip; N = 640: a
+    4th block of 2 strips. Against an fp64 reference on at most 512 particles:
     every element within bf16 output rounding plus the bf16 probabilities' error, and no non-finite value anywhere
     (the round-2 stale-register NaN). q_rows = 1 (the CLS kernel) likewise."""
     torch.manual_seed(N + H)
@@ -589,9 +592,10 @@ def test_attention_bf16_rescale_branch():
     """The lazy online-softmax rescale only runs when a query's max grows by > 2^8 (exp2 domain) within a
     key tile: force it (a key row aligned with a query, late in the sequence) and also plant spikes below the
     threshold, then check against a full fp64 reference (cdna_hip_programming.md §5.4 rule 26), on the key-pipelined
-    kernel (N = 197) and the whole-image one (N = 300)."""
+    kernel (N = 197) and the key-streamed one (N = 300, 577). Since round 5 a step exponentiates against the running
+    max first and redoes the step only when a lane's probabilities sum past 2^8: the spike rows force that redo."""
     torch.manual_seed(26)
-    for B, N, H in ((100, 197, 12), (40, 300, 12)):
+    for B, N, H in ((100, 197, 12), (40, 300, 12), (40, 577, 16)):
         D = 64 * H
         qkv = (torch.randn(B, N, 3 * D, device=DEV) * 0.5).to(torch.bfloat16)
         for b in range(0, B, 7):

@@ -61,10 +61,6 @@ __device__ __forceinline__ float xor32_sum(float x) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// One key step of T 32-key tiles (T = 1 or 2) for a 32-query strip: S^T = K Q^T on MFMA, online softmax
-// update of (m, l, O), O^T += V^T P^T with V^T fragments from transposed LDS reads. MASK: this step contains
-// padded keys (only the last step). The O / l rescale is skipped when no query's running max moved in this
-// step (wave-uniform test), which is the common case after the first key tiles.
 // ds_read_b64_tr_b16 as inline asm: hipcc treats the builtin as a possible reader of in-flight LDS-DMA
 // bytes and drains vmcnt(0) before it, which would serialise the key-pipelined kernel on its last chunk.
 // The caller waits lgkmcnt itself (tr_wait) before the MFMA that consumes the result.
@@ -76,197 +72,6 @@ __device__ __forceinline__ bf16x4 ds_read_tr_asm_o(uint32_t addr) {
     bf16x4 r;
     asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
     return r;
-}
-
-// PRE (ASM_TR only): the four K fragment reads are issued together ahead of the QK^T MFMAs (one lgkmcnt wait instead of
-// four read -> wait -> MFMA pairs; profiles/r3_lab/attn_pre_stagger_ab.txt).
-template <int T, bool MASK, bool ASM_TR = false, bool PRE = false>
-__device__ __forceinline__ void attn_step(const char* Ks, const char* Vs, int kb, int N, int lane, const bf16x8 qf[4],
-                                          float scale_log2, float& m, float& l, f32x16& o0, f32x16& o1) {
-    static_assert(!PRE || (ASM_TR && T == 1), "PRE: the one-tile asm transposed-read step");
-    const int l32 = lane & 31, hh = lane >> 5;
-    f32x16 s[T];
-    bf16x4 vr[2][2][2];
-    if constexpr (PRE) {
-        s[0] = f32x16{};
-        const int kr = kb + l32;
-        bf16x8 kf[4];
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], qf[ks], s[0], 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        __builtin_amdgcn_sched_barrier(0);
-    } else {
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        s[t] = f32x16{};
-        const int kr = kb + t * 32 + l32;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
-            s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[t], 0, 0, 0);
-        }
-    }
-    }
-    float bm = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if constexpr (MASK) {
-                const int key = kb + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                if (key >= N) s[t][r] = -INFINITY;
-            }
-            bm = fmaxf(bm, s[t][r]);
-        }
-    bm = xor32_max(bm);
-    // Lazy rescale (T13): the running max m only moves when some query's tile max exceeds it by more than
-    // 8 in the exp2 domain, so probabilities stay <= 2^8 (exact in fp32 accumulation, representable in bf16)
-    // and the O / l rescale is skipped on almost every tile. The first tile always sets m (m = -inf).
-    if (__builtin_expect(__any(bm > m + 8.0f / scale_log2), 0)) {   // loop-invariant threshold: 2 VALU, not 3
-        const float mn = fmaxf(m, bm);
-        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
-        m = mn;
-        l *= alpha;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            o0[r] *= alpha;
-            o1[r] *= alpha;
-        }
-    }
-    const float msc = m * scale_log2;
-    bf16x8 pf[T][2];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(s[t][r], scale_log2, -msc));
-            s[t][r] = p;
-            l += p;
-        }
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            const uint4 u = make_uint4(pack_bf2(s[t][8 * st + 0], s[t][8 * st + 1]), pack_bf2(s[t][8 * st + 2], s[t][8 * st + 3]),
-                                       pack_bf2(s[t][8 * st + 4], s[t][8 * st + 5]), pack_bf2(s[t][8 * st + 6], s[t][8 * st + 7]));
-            pf[t][st] = __builtin_bit_cast(bf16x8, u);
-        }
-    }
-    const int grp = lane >> 4, gi = lane & 15;
-    const int rq = gi >> 2, cp = gi & 3;
-    if constexpr (ASM_TR) {
-        static_assert(T == 1, "asm transposed-read path handles one 32-key tile");
-        const int rbase = kb + 4 * (grp >> 1) + rq;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
-            const int c16 = col >> 3, inner = (col & 7) * 2;
-            const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, c16) + inner);
-            vr[0][dt][0] = ds_read_tr_asm_o<0>(a);
-            vr[0][dt][1] = ds_read_tr_asm_o<1024>(a);
-            vr[1][dt][0] = ds_read_tr_asm_o<2048>(a);
-            vr[1][dt][1] = ds_read_tr_asm_o<3072>(a);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1]),
-                     "+v"(vr[1][0][0]), "+v"(vr[1][0][1]), "+v"(vr[1][1][0]), "+v"(vr[1][1][1])::"memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt) {
-                const bf16x4 lo = vr[st][dt][0], hi = vr[st][dt][1];
-                const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][st], o0, 0, 0, 0);
-                else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][st], o1, 0, 0, 0);
-            }
-        return;
-    }
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            const int rbase = kb + t * 32 + st * 16 + 4 * (grp >> 1) + rq;
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt) {
-                const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
-                const int c16 = col >> 3, inner = (col & 7) * 2;
-                const bf16x4 lo = ds_read_tr(Vs, v_off(rbase, c16) + inner);
-                const bf16x4 hi = ds_read_tr(Vs, v_off(rbase + 8, c16) + inner);
-                const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][st], o0, 0, 0, 0);
-                else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][st], o1, 0, 0, 0);
-            }
-        }
-}
-
-// The last key step when at most 8 keys of its 32 are real (N - kb <= 8: N = 197 -> 5 keys, N = 577 -> 1).
-// Lane (l32, hh) holds key offsets (r & 3) + 8 (r >> 2) + 4 hh in s[r], so only r = 0..3 can be real: the
-// max / exp / sum run on those 4 (12 of 16 registers are dead, and only their 4 need the key < N test),
-// the probabilities of keys 8..31 are 0, and the second 16-key PV half (st = 1) is skipped. Padded K / V rows
-// are copies of row N - 1 (finite), so the zero probabilities add exactly nothing, as in attn_step<MASK>.
-__device__ __forceinline__ void attn_step_tail8(const char* Ks, const char* Vs, int kb, int N, int lane,
-                                                const bf16x8 qf[4], float scale_log2, float& m, float& l,
-                                                f32x16& o0, f32x16& o1) {
-    // the lane id re-read through asm: its address math then stays inside this (last) step instead of being
-    // hoisted above the key loop, where it held ~40 extra VGPRs and spilled
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    const int l32 = lane & 31, hh = lane >> 5;
-    f32x16 s = f32x16{};
-    const int kr = kb + l32;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, ks * 2 + hh));
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s, 0, 0, 0);
-    }
-    float sv[4];
-    float bm = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        sv[r] = kb + r + 4 * hh < N ? s[r] : -INFINITY;
-        bm = fmaxf(bm, sv[r]);
-    }
-    bm = xor32_max(bm);
-    if (__builtin_expect(__any(bm > m + 8.0f / scale_log2), 0)) {   // loop-invariant threshold: 2 VALU, not 3
-        const float mn = fmaxf(m, bm);
-        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
-        m = mn;
-        l *= alpha;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            o0[r] *= alpha;
-            o1[r] *= alpha;
-        }
-    }
-    const float msc = m * scale_log2;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        sv[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], scale_log2, -msc));
-        l += sv[r];
-    }
-    const uint4 u = make_uint4(pack_bf2(sv[0], sv[1]), pack_bf2(sv[2], sv[3]), 0u, 0u);
-    const bf16x8 pf = __builtin_bit_cast(bf16x8, u);
-    const int grp = lane >> 4, gi = lane & 15;
-    const int rq = gi >> 2, cp = gi & 3;
-    bf16x4 vr[2][2];
-    const int rbase = kb + 4 * (grp >> 1) + rq;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-        const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
-        const int c16 = col >> 3, inner = (col & 7) * 2;
-        const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(rbase, c16) + inner);
-        vr[dt][0] = ds_read_tr_asm_o<0>(a);
-        vr[dt][1] = ds_read_tr_asm_o<1024>(a);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0]), "+v"(vr[0][1]), "+v"(vr[1][0]), "+v"(vr[1][1])::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-        const bf16x4 lo = vr[dt][0], hi = vr[dt][1];
-        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o0, 0, 0, 0);
-        else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o1, 0, 0, 0);
-    }
 }
 
 // 16-query strip on v_mfma_f32_16x16x32_bf16: the last strip when it holds at most 16 real queries (N = 197 ->
@@ -294,18 +99,19 @@ __device__ __forceinline__ float xor16_sum(float x) {
 }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Kt / Vt: the tile's first K / V row in LDS; kb: its first key index (masking only).
 template <bool MASK>
-__device__ __forceinline__ void attn_step16(const char* Ks, const char* Vs, int kb, int N, int lane, const bf16x8 qf[2],
+__device__ __forceinline__ void attn_step16(const char* Kt, const char* Vt, int kb, int N, int lane, const bf16x8 qf[2],
                                             float scale_log2, float& m, float& l, f32x4 (&o)[4]) {
     const int r16 = lane & 15, g = lane >> 4;
     f32x4 s[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
         s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int kr = kb + 16 * kt + r16;
+        const int kr = 16 * kt + r16;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(kr, 4 * kk + g));
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kt + k_off(kr, 4 * kk + g));
             s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], s[kt], 0, 0, 0);
         }
     }
@@ -347,7 +153,7 @@ __device__ __forceinline__ void attn_step16(const char* Ks, const char* Vs, int 
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
         const int c16 = 2 * dt + (p4 >> 1), inner = 8 * (p4 & 1);
-        const uint32_t a = (uint32_t)(size_t)Vs + (uint32_t)(v_off(kb + 4 * g + q, c16) + inner);
+        const uint32_t a = (uint32_t)(size_t)Vt + (uint32_t)(v_off(4 * g + q, c16) + inner);
         vr[dt][0] = ds_read_tr_asm_o<0>(a);
         vr[dt][1] = ds_read_tr_asm_o<2048>(a);
     }
@@ -362,81 +168,252 @@ __device__ __forceinline__ void attn_step16(const char* Ks, const char* Vs, int 
     }
 }
 
-// One workgroup per (particle, head); one wave per 32-query strip (up to 8 waves, strips beyond loop).
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_bf16(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                   int N, int H, float scale_log2, int q_rows) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int NP = (N + 31) & ~31;       // keys padded to whole 32-key MFMA tiles
-    char* Ks = smem;
-    char* Vs = smem + NP * ROWB;
-    const int bh = blockIdx.x;
-    const int b = bh / H, h = bh - (bh / H) * H;
-    const int D = H * HD;
-    const int64_t row0 = (int64_t)b * N;
-    const bf16_t* qbase = qkv + row0 * 3 * D + h * HD;
-    const bf16_t* kbase = qbase + D;
-    const bf16_t* vbase = qbase + 2 * D;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
-
-    // K/V staging: every DMA piece (8 rows x 128 B per wave-instruction, swizzle applied on the source
-    // address, lane-linear LDS destination) is in flight at once, and the first strip's Q loads are issued
-    // under it. Rows >= N are filled from row N-1: finite values whose keys are masked (probability 0).
-    {
-        const int ninstr = NP >> 3, sub = lane >> 3, slot = lane & 7;
-        for (int j = wid; j < 2 * ninstr; j += nw) {
-            const bool isv = j >= ninstr;
-            const int g = isv ? j - ninstr : j;
-            const int r = 8 * g + sub;
-            const int c = isv ? (slot ^ (((r >> 1) & 1) << 2)) : (slot ^ ((r >> 1) & 7));
-            const bf16_t* src = (isv ? vbase : kbase) + (int64_t)min(r, N - 1) * 3 * D + c * 8;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)((isv ? Vs : Ks) + g * 1024), 16, 0, 0);
-        }
-    }
-    const int l32 = lane & 31, hh = lane >> 5;
-    const int nstrips = (q_rows + 31) >> 5;
-    bf16x8 q0[4];
-    {
-        const int q = min(wid * 32 + l32, N - 1);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) q0[ks] = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)q * 3 * D + ks * 16 + hh * 8);
-    }
-    __syncthreads();
-
-    for (int strip = wid; strip < nstrips; strip += nw) {
-        const int q = strip * 32 + l32;
-        bf16x8 qf[4];
-        if (strip == wid) {
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) qf[ks] = q0[ks];
-        } else {
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
-                qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)min(q, N - 1) * 3 * D + ks * 16 + hh * 8);
-        }
-        f32x16 o0 = {}, o1 = {};
-        float m = -INFINITY, l = 0.f;
-        // full 32-key tiles need no mask; only the tail tile (NP - N padded keys) is masked. One S tile live
-        // keeps the kernel at <= 128 VGPRs = 4 waves/SIMD (two 7-wave workgroups per CU).
-        const int nfull = N & ~31;
-        int kb = 0;
-        for (; kb < nfull; kb += 32) attn_step<1, false>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
-        if (kb < NP) attn_step<1, true>(Ks, Vs, kb, N, lane, qf, scale_log2, m, l, o0, o1);
-        l = xor32_sum(l);
-        const float inv = 1.0f / l;
-        if (q < q_rows) {
-            bf16_t* orow = out + (row0 + q) * D + h * HD;
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const int d = 8 * g4 + 4 * hh;
-                *reinterpret_cast<uint2*>(orow + d) =
-                    make_uint2(pack_bf2(o0[4 * g4] * inv, o0[4 * g4 + 1] * inv), pack_bf2(o0[4 * g4 + 2] * inv, o0[4 * g4 + 3] * inv));
-                *reinterpret_cast<uint2*>(orow + 32 + d) =
-                    make_uint2(pack_bf2(o1[4 * g4] * inv, o1[4 * g4 + 1] * inv), pack_bf2(o1[4 * g4 + 2] * inv, o1[4 * g4 + 3] * inv));
-            }
-        }
-    }
+// ---------------- round 5: the row sum on the matrix cores, and a speculative running max ----------------
+// Per 32-key step a 32-query strip spent ~490 issue cycles per wave against 256 cycles of MFMA work (8 x 32x32x16):
+// 16 v_exp_f32 (8 cyc each), 16 v_fma_f32 (the exp2 argument), 16 v_add_f32 (the row sum l), 8 v_max3_f32 + a permlane
+// swap + compare (the running max), 8 v_cvt_pk_bf16_f32, address adds (MI355X_MICROARCH.md 'vector-instruction ISSUE
+// cost'). Two of those groups move off the vector issue port here:
+//  * l: each lane's bf16-packed probabilities (the PV MFMA's B operand) are summed by v_mfma_f32_4x4x4_16b_bf16 against
+//    a ones A operand (four per step: 4 values per lane each, every accumulator register gets the lane's own sum), so
+//    the 16 v_add_f32 become 4 MFMA issues. l is then the sum of the very bf16 weights the PV MFMA multiplies.
+//  * the running max: the step exponentiates against the current m without looking for a new maximum, and the
+//    accumulated l tells whether that was safe: a lane whose 16 probabilities sum to at most 2^8 has none above 2^8,
+//    the bound the lazy rescale (T13) already allowed. Only when some lane's step sum exceeds it (or is not finite) does
+//    the step recompute its scores, take the max, rescale O and l and exponentiate again (rare after the first keys).
+//    The first key step of a strip takes the max as before (m = -inf).
+__device__ __forceinline__ f32x4 lsum8(const bf16x8 p, f32x4 acc) {
+    const bf16x4 ones = {(short)0x3F80, (short)0x3F80, (short)0x3F80, (short)0x3F80};
+    const bf16x4 lo = __builtin_shufflevector(p, p, 0, 1, 2, 3);
+    const bf16x4 hi = __builtin_shufflevector(p, p, 4, 5, 6, 7);
+    acc = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(ones, lo, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(ones, hi, acc, 0, 0, 0);
 }
 
+__device__ __forceinline__ float max16(const f32x16& s) {
+    float bm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bm = fmaxf(bm, s[r]);
+    return bm;
+}
+
+// S^T = K Q^T for one 32-key tile: the four K fragment reads together, then the four MFMAs (attn_step's PRE form)
+// Kt: the tile's first K row in LDS (the swizzles depend on the row's low bits only, so a 32-row tile is addressed by
+// its local rows)
+__device__ __forceinline__ f32x16 qk32(const char* Kt, int lane, const bf16x8 qf[4]) {
+    const int l32 = lane & 31, hh = lane >> 5;
+    f32x16 s = f32x16{};
+    bf16x8 kf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(Kt + k_off(l32, ks * 2 + hh));
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], qf[ks], s, 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    return s;
+}
+
+// O^T += V^T P^T over one 32-key tile (both 16-key halves when HALVES == 2; the tail step's first half only when 1)
+template <int HALVES>
+__device__ __forceinline__ void pv32(const char* Vt, int lane, const bf16x8 pf[2], f32x16& o0, f32x16& o1) {
+    const int grp = lane >> 4, gi = lane & 15;
+    const int rq = gi >> 2, cp = gi & 3;
+    const int rbase = 4 * (grp >> 1) + rq;
+    bf16x4 vr[2][2][2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
+        const int c16 = col >> 3, inner = (col & 7) * 2;
+        const uint32_t a = (uint32_t)(size_t)Vt + (uint32_t)(v_off(rbase, c16) + inner);
+        vr[0][dt][0] = ds_read_tr_asm_o<0>(a);
+        vr[0][dt][1] = ds_read_tr_asm_o<1024>(a);
+        if constexpr (HALVES == 2) {
+            vr[1][dt][0] = ds_read_tr_asm_o<2048>(a);
+            vr[1][dt][1] = ds_read_tr_asm_o<3072>(a);
+        }
+    }
+    if constexpr (HALVES == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1]),
+                     "+v"(vr[1][0][0]), "+v"(vr[1][0][1]), "+v"(vr[1][1][0]), "+v"(vr[1][1][1])::"memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1])
+                     ::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int st = 0; st < HALVES; ++st)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const bf16x4 lo = vr[st][dt][0], hi = vr[st][dt][1];
+            const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o0, 0, 0, 0);
+            else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o1, 0, 0, 0);
+        }
+}
+
+// The same step in the rounds 1-4 form (the N <= 256 kernel's): the row max of every tile (T13 lazy rescale when it
+// moved by more than 2^8), l summed from the fp32 probabilities. Bit-identical to the rounds 1-4 attn_step.
+template <bool MASK>
+__device__ __forceinline__ void attn_step_pl(const char* Kt, const char* Vt, int kb, int N, int lane, const bf16x8 qf[4],
+                                             float scale_log2, float& m, float& l, f32x16& o0, f32x16& o1) {
+    const int hh = lane >> 5;
+    f32x16 s = qk32(Kt, lane, qf);
+    float bm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        if constexpr (MASK) {
+            if (kb + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) s[r] = -INFINITY;
+        }
+        bm = fmaxf(bm, s[r]);
+    }
+    bm = xor32_max(bm);
+    if (__builtin_expect(__any(bm > m + 8.0f / scale_log2), 0)) {   // loop-invariant threshold: 2 VALU, not 3
+        const float mn = fmaxf(m, bm);
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        m = mn;
+        l *= alpha;
+        o0 *= alpha;
+        o1 *= alpha;
+    }
+    const float msc = m * scale_log2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], scale_log2, -msc));
+        s[r] = p;
+        l += p;
+    }
+    bf16x8 pf[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+        pf[st] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(s[8 * st + 0], s[8 * st + 1]), pack_bf2(s[8 * st + 2], s[8 * st + 3]),
+                                                       pack_bf2(s[8 * st + 4], s[8 * st + 5]), pack_bf2(s[8 * st + 6], s[8 * st + 7])));
+    pv32<2>(Vt, lane, pf, o0, o1);
+}
+
+// attn_step_tail8 of rounds 1-4 (at most 8 real keys in the tile: s[0..3] only, the first 16-key PV half)
+__device__ __forceinline__ void attn_step_tail8_pl(const char* Kt, const char* Vt, int kb, int N, int lane,
+                                                   const bf16x8 qf[4], float scale_log2, float& m, float& l,
+                                                   f32x16& o0, f32x16& o1) {
+    // the lane id re-read through asm: its address math then stays inside this (last) step instead of being
+    // hoisted above the key loop, where it held ~40 extra VGPRs and spilled
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int hh = lane >> 5;
+    const f32x16 s = qk32(Kt, lane, qf);
+    float sv[4];
+    float bm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sv[r] = kb + r + 4 * hh < N ? s[r] : -INFINITY;
+        bm = fmaxf(bm, sv[r]);
+    }
+    bm = xor32_max(bm);
+    if (__builtin_expect(__any(bm > m + 8.0f / scale_log2), 0)) {
+        const float mn = fmaxf(m, bm);
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        m = mn;
+        l *= alpha;
+        o0 *= alpha;
+        o1 *= alpha;
+    }
+    const float msc = m * scale_log2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sv[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], scale_log2, -msc));
+        l += sv[r];
+    }
+    bf16x8 pf[2];
+    pf[0] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(sv[0], sv[1]), pack_bf2(sv[2], sv[3]), 0u, 0u));
+    pf[1] = bf16x8{};
+    pv32<1>(Vt, lane, pf, o0, o1);
+}
+
+// One 32-key step of a 32-query strip with l on the matrix cores and the speculative max (above). Kt / Vt: the tile's
+// first K / V row in LDS; kb: its first key index (masking only). `first`: the strip's first key step (m = -inf: take
+// the tile max). MASK: keys >= N in this tile get probability 0. lacc: the 4x4x4 MFMA accumulator (every register = the
+// lane's running l).
+template <bool MASK>
+__device__ __forceinline__ void attn_step_lf(const char* Kt, const char* Vt, int kb, int N, int lane, const bf16x8 qf[4],
+                                             float scale_log2, bool first, float& m, f32x4& lacc, f32x16& o0,
+                                             f32x16& o1) {
+    const int hh = lane >> 5;
+    auto mask = [&](f32x16& t) {
+        if constexpr (MASK) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (kb + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) t[r] = -INFINITY;
+        }
+    };
+    f32x16 s = qk32(Kt, lane, qf);
+    mask(s);
+    if (first) m = xor32_max(max16(s));
+    bf16x8 pf[2];
+    f32x4 ln;
+    auto expo = [&](f32x16& t) {   // t: scores in, probabilities out
+        const float msc = m * scale_log2;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t[r] = __builtin_amdgcn_exp2f(fmaf(t[r], scale_log2, -msc));
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+            pf[st] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(t[8 * st + 0], t[8 * st + 1]),
+                                                           pack_bf2(t[8 * st + 2], t[8 * st + 3]),
+                                                           pack_bf2(t[8 * st + 4], t[8 * st + 5]),
+                                                           pack_bf2(t[8 * st + 6], t[8 * st + 7])));
+        ln = lsum8(pf[1], lsum8(pf[0], lacc));
+    };
+    expo(s);
+    if (!first && __builtin_expect(__any(!(ln[0] - lacc[0] <= 256.0f)), 0)) {
+        f32x16 t = qk32(Kt, lane, qf);   // the scores again (s holds probabilities now)
+        mask(t);
+        const float mn = fmaxf(m, xor32_max(max16(t)));
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        m = mn;
+        lacc *= alpha;
+        o0 *= alpha;
+        o1 *= alpha;
+        expo(t);
+    }
+    lacc = ln;
+    pv32<2>(Vt, lane, pf, o0, o1);
+}
+
+// The last key step when at most 8 of its 32 keys are real (attn_step_tail8's register map: s[0..3] only), in the
+// attn_step_lf form: one 4x4x4 MFMA for l, the speculative max, the first 16-key PV half.
+__device__ __forceinline__ void attn_step_tail8_lf(const char* Kt, const char* Vt, int kb, int N, int lane,
+                                                   const bf16x8 qf[4], float scale_log2, bool first, float& m,
+                                                   f32x4& lacc, f32x16& o0, f32x16& o1) {
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int hh = lane >> 5;
+    const f32x16 s = qk32(Kt, lane, qf);
+    float sv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sv[r] = kb + r + 4 * hh < N ? s[r] : -INFINITY;
+    auto max4 = [&]() { return xor32_max(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3]))); };
+    if (first) m = max4();
+    bf16x8 pf[2];
+    pf[1] = bf16x8{};
+    f32x4 ln;
+    auto expo = [&]() {
+        const float msc = m * scale_log2;
+        float p[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], scale_log2, -msc));
+        pf[0] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]), 0u, 0u));
+        const bf16x4 ones = {(short)0x3F80, (short)0x3F80, (short)0x3F80, (short)0x3F80};
+        ln = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(ones, __builtin_shufflevector(pf[0], pf[0], 0, 1, 2, 3), lacc, 0,
+                                                    0, 0);
+    };
+    expo();
+    if (!first && __builtin_expect(__any(!(ln[0] - lacc[0] <= 256.0f)), 0)) {
+        const float mn = fmaxf(m, max4());
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        m = mn;
+        lacc *= alpha;
+        o0 *= alpha;
+        o1 *= alpha;
+        expo();
+    }
+    lacc = ln;
+    pv32<1>(Vt, lane, pf, o0, o1);
+}
 
 // s_waitcnt vmcnt(n) for a runtime n (the immediate must be a constant): n >= the outstanding count is a no-op
 __device__ __forceinline__ void wait_vmcnt(int n) {
@@ -492,12 +469,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31, hh = lane >> 5;
     const int nstrips = (q_rows + 31) >> 5;
+    // sid: this wave's query strip (the identity; round 5 tried swapping waves 4, 5 with 6, 7 in every other workgroup so
+    // that the half-work and idle strips of two co-resident workgroups land on different SIMDs: 1.4 % slower,
+    // profiles/r5_lab/attn_simd_balance_ab.txt)
+    const int sid = wid;
     // wave-uniform: this wave's strip holds query N - 1 and at most 16 real queries. Decided by N, not q_rows, so a
     // row's result does not depend on how many rows the call computes.
     const int nlast = (N - 1) >> 5;
     constexpr bool TAIL8 = true;
-    const bool w16 = !OUT8 && wid == nlast && wid < nstrips && N - 32 * nlast <= 16;
-    const int q = wid * 32 + l32;
+    const bool w16 = !OUT8 && sid == nlast && sid < nstrips && N - 32 * nlast <= 16;
+    const int q = sid * 32 + l32;
     // Q fragments by inline-asm loads: hipcc does not count them, so it cannot merge them into a vmcnt(0) at
     // the first MFMA (which would also drain every K/V chunk). They are older than all DMA pieces, so the
     // first chunk's counted wait retires them; the empty asm after it pins every use below that wait.
@@ -509,7 +490,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // on the 32-query strips too).
     bf16x8 qf[4];
     {
-        const bf16_t* qp = w16 ? qbase + (int64_t)min(wid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
+        const bf16_t* qp = w16 ? qbase + (int64_t)min(sid * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
                                : qbase + (int64_t)min(q, N - 1) * 3 * D + hh * 8;
         const int step = w16 ? 32 : 16;
 #pragma unroll
@@ -538,7 +519,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // or merge between an asm load and the wait that retires it; the wait carries no register operands.)
     wait_vmcnt(NT);
     asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
-    const bool active = wid < nstrips;
+    const bool active = sid < nstrips;
     const int nfull = N >> 5;             // chunks without padded keys
     // The chunk loop, one template for both strip kinds: the barrier schedule (a counted wait + s_barrier before
     // chunks 0, CPB, 2 CPB, ..., and before the padded tail chunk) depends on N and CPB only.
@@ -556,8 +537,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                 pin_q();
             }
             if (active) {
-                if constexpr (W16) attn_step16<false>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
-                else attn_step<1, false, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                if constexpr (W16) attn_step16<false>(Ks + c * 4096, Vs + c * 4096, c * 32, N, lane, qf, scale_log2, m, l, o16);
+                else attn_step_pl<false>(Ks + c * 4096, Vs + c * 4096, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
             }
         }
         if (c < NT) {
@@ -567,9 +548,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                 pin_q();
             }
             if (active) {
-                if constexpr (W16) attn_step16<true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o16);
-                else if (TAIL8 && N - c * 32 <= 8) attn_step_tail8(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-                else attn_step<1, true, true, true>(Ks, Vs, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                if constexpr (W16) attn_step16<true>(Ks + c * 4096, Vs + c * 4096, c * 32, N, lane, qf, scale_log2, m, l, o16);
+                else if (TAIL8 && N - c * 32 <= 8)
+                    attn_step_tail8_pl(Ks + c * 4096, Vs + c * 4096, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                else attn_step_pl<true>(Ks + c * 4096, Vs + c * 4096, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
             }
         }
     };
@@ -581,7 +563,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         // the 4 lanes lane % 16 + 16 g share query 32 wid + lane % 16; lane holds dims 16 dt + 4g .. +3
         l = xor32_sum(xor16_sum(l));
         const float inv = 1.0f / l;
-        const int qq = wid * 32 + (lane & 15);
+        const int qq = sid * 32 + (lane & 15);
         if (qq < q_rows) {
             bf16_t* orow = out + (row0 + qq) * D + h * HD + 4 * (lane >> 4);
 #pragma unroll
@@ -644,6 +626,183 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
 }
 
+
+// ---------------- N > 256 (ViT-L/14 @ 336: N = 577): K / V streamed through a ring, queries in blocks ----------------
+// The N <= 256 kernel keeps a head's whole K / V image in LDS (57 KiB at N = 197); at N = 577 that image is 152 KiB, so
+// one workgroup fits a CU, its load phase is not overlapped, and 19 strips over 8 waves leave the SIMDs unbalanced
+// (round 1-4: 9.93 ms per launch at 4096 x 16 heads = 0.225 of the bf16 peak). Here:
+//  * one workgroup = WAVES (6) waves = one 192-query block of one (particle, head): QB = 3 blocks cover the 576 queries
+//    of the 18 full 32-query strips. The 16-query strip (N = 577: query 576 alone) rides on wave 0 of the last block
+//    (attn_step16 beside its 32-query strip) or on a wave of that block that has no 32-query strip.
+//  * K / V arrive in 32-key chunks (4 KiB of K + 4 KiB of V) through a ring of 9 chunk slots (72 KiB: two workgroups
+//    per CU, 12 waves = 3 per SIMD, 168 VGPRs per wave). A group of 3 chunks = 24 LDS-DMA pieces of 1 KiB, 4 per wave;
+//    three groups are resident: while one is computed, the next two are in flight. One counted vmcnt + s_barrier per
+//    group; after the barrier of group g every wave has finished group g - 1, whose slots take group g + 2.
+//  * the three blocks of a unit run on one XCD (blockIdx b -> XCD b % 8; consecutive blocks of that XCD are one unit's
+//    blocks), so two of the three K / V reads of a unit are L2 hits.
+//  * the steps are attn_step_lf (l on the matrix cores, speculative max), addressed by slot.
+// Per unit the work is 18 strips x 19 key steps (+ the 16-query strip); a row's bits depend on N only, not on q_rows
+// or on the block it falls in.
+// WAVES x CPB: 4 x 2 (product: a 4-wave workgroup has one wave on each SIMD whatever the dispatcher does, 3 workgroups
+// of 48 KiB per CU) or 6 x 3 (72 KiB, 2 per CU); LF: the attn_step_lf steps (else attn_step_pl). Compile-time choices
+// (lab A/B builds define them), not run-time knobs.
+#ifndef VPF_STREAM_WAVES
+#define VPF_STREAM_WAVES 4
+#endif
+#ifndef VPF_STREAM_LF
+#define VPF_STREAM_LF 1
+#endif
+constexpr int STREAM_WAVES = VPF_STREAM_WAVES;
+constexpr int STREAM_CPB = STREAM_WAVES == 4 ? 2 : 3;   // 32-key chunks per group (8 pieces each: 4 per wave per group)
+constexpr int STREAM_RING = 3;                     // groups resident in the ring
+
+template <int WAVES, int CPB, bool LF>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void k_attn_stream(
+    const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows, int QB,
+    int BH) {
+    constexpr int STREAM_CPB = CPB;
+    constexpr int STREAM_SLOTS = CPB * STREAM_RING;
+    constexpr int STREAM_LDS = STREAM_SLOTS * 2 * 4096;
+    static_assert((STREAM_CPB * 8) % WAVES == 0, "a group's DMA pieces split evenly over the waves");
+    constexpr int PPW = STREAM_CPB * 8 / WAVES;    // DMA pieces per wave per group
+    __shared__ __attribute__((aligned(16))) char smem[STREAM_LDS];
+    char* Ks = smem;
+    char* Vs = smem + STREAM_SLOTS * 4096;
+    const int xcd = blockIdx.x & 7, w8 = blockIdx.x >> 3;
+    const int u = (w8 / QB) * 8 + xcd, qb = w8 - (w8 / QB) * QB;
+    if (u >= BH) return;                           // padding of the XCD-grouped grid: the whole workgroup leaves
+    const int b = u / H, h = u - (u / H) * H;
+    const int D = H * HD;
+    const int64_t row0 = (int64_t)b * N;
+    const bf16_t* qbase = qkv + row0 * 3 * D + h * HD;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l32 = lane & 31, hh = lane >> 5;
+    const int NT = (N + 31) >> 5;                  // 32-key chunks
+    const int NG = (NT + STREAM_CPB - 1) / STREAM_CPB;
+    const int SF = N >> 5, tail = N & 31;
+    const int SF32 = SF + (tail > 16 ? 1 : 0);     // 32-query strips (the last one partial when tail > 16)
+    const int st = qb * WAVES + wid;
+    const bool act32 = st < SF32 && st * 32 < q_rows;
+    const int idle0 = SF32 - (QB - 1) * WAVES;     // first wave of the last block without a 32-query strip
+    const bool act16 = tail >= 1 && tail <= 16 && 32 * SF < q_rows && qb == QB - 1 && wid == (idle0 < WAVES ? idle0 : 0);
+
+    // Q fragments by inline-asm loads, unconditionally for both strip kinds (addresses clamped): no branch or merge
+    // between an asm load and the wait that retires it (the rule behind the round-2 / round-4 NaNs, k_attn_bf16_pipe).
+    bf16x8 qf[4], q16[2];
+    {
+        const bf16_t* qp = qbase + (int64_t)min(st * 32 + l32, N - 1) * 3 * D + hh * 8;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + ks * 16));
+        const bf16_t* qp16 = qbase + (int64_t)min(SF * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(q16[kk]) : "v"(qp16 + kk * 32));
+    }
+    // group g = chunks [3g, 3g + 3): piece pi = 0..23 of a group is chunk pi / 8, K (pi & 4 == 0) or V, rows 8 (pi & 3) ..
+    // + 7 of that chunk (one 1 KiB wave-instruction, lane-linear destination, swizzle on the source address as in
+    // k_attn_bf16_pipe); wave w issues pieces w, w + WAVES, ... Rows >= N read row N - 1 (finite; masked keys).
+    auto issue_group = [&](int g) {
+        // the lane id re-read through asm: the pieces' addresses are then computed where they are issued instead of
+        // being hoisted above the group loop as invariants (which spilled, and a scratch reload's vmcnt wait would
+        // drain the DMA stream)
+        int ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        const int sub = ln >> 3, slot = ln & 7;
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+            const int pi = wid + WAVES * i;
+            const int cc = pi >> 3, isv = (pi >> 2) & 1, j = pi & 3;
+            const int c = g * STREAM_CPB + cc;
+            const int r = c * 32 + 8 * j + sub;
+            const int ch = isv ? (slot ^ (((r >> 1) & 1) << 2)) : (slot ^ ((r >> 1) & 7));
+            const int sl = c % STREAM_SLOTS;
+            __builtin_amdgcn_global_load_lds(
+                (gptr_t)(qbase + (isv ? 2 * D : D) + (int64_t)min(r, N - 1) * 3 * D + ch * 8),
+                (lptr_t)((isv ? Vs : Ks) + sl * 4096 + j * 1024), 16, 0, 0);
+        }
+    };
+    const int g0 = min(NG, STREAM_RING);
+    for (int g = 0; g < g0; ++g) issue_group(g);
+    // the Q loads are older than every DMA piece: landed once at most PPW * g0 pieces are outstanding; wait and pin here
+    wait_vmcnt(PPW * g0);
+    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(q16[0]), "+v"(q16[1]) :: "memory");
+
+    f32x16 o0 = {}, o1 = {};
+    f32x4 lacc = {};
+    float m = -INFINITY, l = 0.f;
+    f32x4 o16[4] = {};
+    float m16 = -INFINITY, l16 = 0.f;
+    const int nfull = N >> 5;                      // chunks without padded keys
+    for (int g = 0; g < NG; ++g) {
+        // this wave's pieces of group g have landed (the groups issued after it stay in flight), then every wave's have
+        const int issued = min(NG, max(STREAM_RING, g + 2));
+        wait_vmcnt(PPW * (issued - g - 1));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(q16[0]), "+v"(q16[1]) :: "memory");
+        if (g >= 1 && g + 2 < NG) issue_group(g + 2);   // into group g - 1's slots, which every wave has finished
+        const int c_end = min((g + 1) * STREAM_CPB, nfull);
+#pragma unroll 1
+        for (int c = g * STREAM_CPB; c < c_end; ++c) {   // the group's chunks without padded keys
+            const int sl = c % STREAM_SLOTS;
+            const char* Kt = Ks + sl * 4096;
+            const char* Vt = Vs + sl * 4096;
+            if (act32) {
+                if constexpr (LF) attn_step_lf<false>(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
+                else attn_step_pl<false>(Kt, Vt, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+            }
+            if (act16) attn_step16<false>(Kt, Vt, c * 32, N, lane, q16, scale_log2, m16, l16, o16);
+        }
+    }
+    if (nfull < NT) {   // the chunk with padded keys: the last one, in the last group (whose barrier has passed)
+        const int c = nfull, sl = c % STREAM_SLOTS;
+        const char* Kt = Ks + sl * 4096;
+        const char* Vt = Vs + sl * 4096;
+        if (act32) {
+            if constexpr (LF) {
+                if (N - c * 32 <= 8) attn_step_tail8_lf(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
+                else attn_step_lf<true>(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
+            } else {
+                if (N - c * 32 <= 8) attn_step_tail8_pl(Kt, Vt, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+                else attn_step_pl<true>(Kt, Vt, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
+            }
+        }
+        if (act16) attn_step16<true>(Kt, Vt, c * 32, N, lane, q16, scale_log2, m16, l16, o16);
+    }
+    if (act16) {   // the 4 lanes lane % 16 + 16 g share query 32 SF + lane % 16; lane holds dims 16 dt + 4g .. +3
+        const float inv = 1.0f / xor32_sum(xor16_sum(l16));
+        const int qq = SF * 32 + (lane & 15);
+        if (qq < q_rows) {
+            bf16_t* orow = out + (row0 + qq) * D + h * HD + 4 * (lane >> 4);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+                *reinterpret_cast<uint2*>(orow + 16 * dt) = make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
+                                                                      pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
+        }
+    }
+    if (!act32) return;
+    const float inv = 1.0f / xor32_sum(LF ? lacc[0] : l);
+    uint32_t gx[8], gy[8];   // as k_attn_bf16_pipe: permlane32 pairs -> one 16-B store per 8-dim pair
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const f32x16& o = k < 4 ? o0 : o1;
+        const int b4 = 4 * (k & 3);
+        gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
+        gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
+    }
+    const int q = st * 32 + l32;
+    uint4 ov[4];
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+        const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
+        ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
+    if (q < q_rows) {
+        bf16_t* orow = out + (row0 + q) * D + h * HD + 8 * hh;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
+    }
+}
 
 // CLS-only attention (q_rows == 1: the last encoder block, whose other query rows feed nothing): one wave
 // per (particle, head), 4 per workgroup, no LDS, so occupancy is set by VGPRs and many heads stream K / V
@@ -810,16 +969,15 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     const int NP = (N + 31) & ~31;
     const size_t lds = (size_t)NP * ROWB * 2;
     const float scale_log2 = scale * 1.44269504088896341f;
-    const int strips = (q_rows + 31) / 32;
     const int64_t BH = B * H;
     if (q_rows == 1) {
         hipLaunchKernelGGL(k_attn_cls_bf16, dim3((unsigned)((BH + 3) / 4)), dim3(256), 0, (hipStream_t)stream, qkv, out,
                            N, H, (int)BH, scale_log2);
         VPF_RETURN_LAUNCH();
     }
-    // N <= 256: the key-pipelined kernel (8 waves, one strip each); N > 256: the whole-image kernel (waves loop over
-    // strips). (Round 4's persistent chunk-ring form is bit-identical but 1.5x slower: tools/gemm_lab/attention_lab.hip,
-    // profiles/r4_lab/attn_ring_ab_v*.txt.)
+    // N <= 256: the key-pipelined kernel (8 waves, one strip each, the head's whole K / V image in LDS); N > 256: the
+    // key-streamed, query-blocked kernel. (Round 4's persistent chunk-ring form of the N <= 256 kernel is bit-identical
+    // but 1.5x slower: tools/gemm_lab/attention_lab.hip, profiles/r4_lab/attn_ring_ab_v*.txt.)
     if (N <= 256) {
         static bool pipe_attr = false;   // benign race: idempotent attribute set
         if (!pipe_attr) {
@@ -832,14 +990,16 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
                            (uint8_t*)nullptr, 0, (uint8_t*)nullptr, 0);
         VPF_RETURN_LAUNCH();
     }
-    const int threads = 64 * (strips < 8 ? strips : 8);
-    static bool attr_set = false;   // benign race: idempotent attribute set
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_attn_bf16, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
-    }
-    hipLaunchKernelGGL(k_attn_bf16, dim3((unsigned)(B * H)), dim3(threads), lds, (hipStream_t)stream, qkv, out, N,
-                       H, scale_log2, q_rows);
+    constexpr int W = STREAM_WAVES;
+    const int sf32 = (N >> 5) + ((N & 31) > 16 ? 1 : 0);
+    const int need = sf32 < (q_rows + 31) / 32 ? sf32 : (q_rows + 31) / 32;   // 32-query strips holding rows < q_rows
+    const int QB = need > W ? (need + W - 1) / W : 1;
+    const int64_t blocks = (BH + 7) / 8 * 8 * QB;
+    if (blocks > INT32_MAX) return VPF_ERR_ARG;
+    hipLaunchKernelGGL((k_attn_stream<W, STREAM_CPB, VPF_STREAM_LF != 0>), dim3((unsigned)blocks), dim3(64 * W), 0,
+                       (hipStream_t)stream,
+                       reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows,
+                       QB, (int)BH);
     VPF_RETURN_LAUNCH();
 }
 
