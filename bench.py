@@ -370,6 +370,11 @@ def main() -> int:
     peak = PEAK_FP8_TFLOPS if args.dtype == "fp8" and dom in ("gemm_qkv", "gemm_fc1", "gemm_fc2") else PEAK_BF16_TFLOPS
     gflop_frame = arch.gflop_per_crop() * args.particles
     gflop_exec = arch.gflop_per_crop_executed(cls_fused=tr.engine.cls_fused) * args.particles
+    gflop_mx8 = arch.gflop_per_crop_mx8() * args.particles if args.dtype == "fp8" else 0.0
+
+    def frame_peak_time(gflop, gflop8):
+        """Seconds the frame's MFMA work takes at the dense peaks (gflop8 of it on MX8 GEMMs)."""
+        return (gflop8 / PEAK_FP8_TFLOPS + (gflop - gflop8) / PEAK_BF16_TFLOPS) * 1e9 / 1e12
     check = multi_rank_check(tr, world, rank, dev, args.dist_backend) if world > 1 else None
     line = {
         "metric": METRIC,
@@ -399,9 +404,15 @@ def main() -> int:
                      "avg_launch_ms": round(ks[dom]["avg_ms"], 4),
                      "flop_per_launch": flops[dom]},
         # full-forward FLOPs (SURVEY §8d's count, what the metric's roofline is quoted on) and the FLOPs of the work
-        # the product actually performs (the last block computes the CLS row only; config.gflop_per_crop_executed)
-        "frame_mfma_frac": round(gflop_frame * 1e9 * fps / (PEAK_BF16_TFLOPS * 1e12 * world), 4),
-        "frame_mfma_frac_executed": round(gflop_exec * 1e9 * fps / (PEAK_BF16_TFLOPS * 1e12 * world), 4),
+        # the product actually performs (the last block computes the CLS row only; config.gflop_per_crop_executed),
+        # each as the fraction of the frame the MFMA work would take at its dense peak: the fp8 path's block-scaled
+        # GEMMs against the fp8 peak, everything else against bf16 (frame_peak_note; VERDICT r4 #6: round 4 divided the
+        # fp8 frame's FLOPs by the bf16 peak alone, which overstated its utilisation ~2x)
+        "frame_mfma_frac": round(fps * frame_peak_time(gflop_frame, gflop_mx8) / world, 4),
+        "frame_mfma_frac_executed": round(fps * frame_peak_time(gflop_exec, gflop_mx8) / world, 4),
+        "frame_peak_note": ("bf16 dense peak" if gflop_mx8 == 0 else
+                            f"FLOP-weighted: {round(gflop_mx8 / args.particles, 4)} GFLOP per crop of MX8 GEMMs at "
+                            f"{PEAK_FP8_TFLOPS:.0f} TF, the rest at {PEAK_BF16_TFLOPS:.0f} TF"),
         "gflop_per_crop": {"full_forward": round(arch.gflop_per_crop(), 4),
                            "executed": round(gflop_exec / args.particles, 4)},
         "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}

@@ -225,6 +225,19 @@ def test_weights_digest_tracks_the_weight_set():
     assert weights_digest(w) != d0
 
 
+def test_fp8_frame_flop_split():
+    """bench.py's fp8 frame fraction weighs the MX8 GEMMs' FLOPs against the fp8 peak: QKV, FC1, FC2 and
+    (N <= 256) proj of blocks 0..L-2 run on MX8; the rest of the executed FLOPs stays bf16."""
+    from vitparticlefiltertracker_amd.config import ARCHS
+    b = ARCHS["vit_base_patch16_224"]
+    N, D, F = b.tokens, b.dim, b.mlp
+    assert abs(b.gflop_per_crop_mx8() - 2 * 11 * (3 * N * D * D + N * D * D + 2 * N * D * F) / 1e9) < 1e-9
+    assert b.gflop_per_crop_mx8() < b.gflop_per_crop_executed() < b.gflop_per_crop()
+    big = ARCHS["vit_large_patch14_336"]                 # N = 577: proj reads the bf16 attention output
+    Nl, Dl, Fl = big.tokens, big.dim, big.mlp
+    assert abs(big.gflop_per_crop_mx8() - 2 * 23 * (3 * Nl * Dl * Dl + 2 * Nl * Dl * Fl) / 1e9) < 1e-9
+
+
 def test_checkpoint_formats_are_refused_with_a_reason():
     """the weights' crc32 joined the fingerprint in round 4, so the format is now 3; format 1 and format 2
     files get an explicit 're-create the checkpoint' message instead of a generic configuration mismatch."""

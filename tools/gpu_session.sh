@@ -72,6 +72,18 @@ for step in "$@"; do
       ok_or_stop $? pmc_mfma
       python tools/pmc_frame.py $OUT/pmc_mfma --frames 3 > $OUT/pmc_mfma_frame.txt 2>&1
       ok_or_stop $? pmc_frame; cat $OUT/pmc_mfma_frame.txt ;;
+    pmc_l)   # PMC traffic of configs[3] (ViT-L/14 @ 336, 4096 particles, bf16): bench.py's roofline.traffic for that line
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmcl_fetch -o p --output-format csv -- python3 bench.py --arch vit_large_patch14_336 --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmcl_fetch.log 2>&1
+      ok_or_stop $? pmcl_fetch
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmcl_write -o p --output-format csv -- python3 bench.py --arch vit_large_patch14_336 --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmcl_write.log 2>&1
+      ok_or_stop $? pmcl_write
+      python tools/pmc_traffic.py $OUT/pmcl_fetch $OUT/pmcl_write --arch vit_large_patch14_336 --particles 4096 --frame 224x224 > $OUT/pmc_traffic_vitl.json 2> $OUT/pmcl_traffic.err
+      ok_or_stop $? pmcl_traffic; head -40 $OUT/pmc_traffic_vitl.json ;;
+    prof_l)   # rocprofv3 kernel stats of configs[3] (ViT-L/14 @ 336)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof_l -o run --output-format csv -- python3 bench.py --arch vit_large_patch14_336 --steps 2 --warmup 1 --cpu-baseline off > $OUT/prof_l.log 2>&1
+      ok_or_stop $? prof_l; tail -1 $OUT/prof_l.log | cut -c1-300 ;;
     pmc8)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc8_fetch -o p --output-format csv -- python3 bench.py --dtype fp8 --steps 1 --warmup 1 --kernel-frames 1 --cpu-baseline off --no-graph > $OUT/pmc8_fetch.log 2>&1

@@ -75,6 +75,14 @@ class ViTArch:
         f = 2 * (n * self.patch_k * D + (L - 1) * full_block + last)
         return f / 1e9
 
+    def gflop_per_crop_mx8(self) -> float:
+        """FLOPs per crop that the fp8 path (model.dtype: fp8) runs on block-scaled MX8 MFMA, in GFLOP: QKV, FC1 and FC2
+        of blocks 0..L-2, and their proj when N <= 256 (the attention then writes MX8; vit.py ViTEngine.encoder). The
+        patch embedding, the attention and the last block stay bf16."""
+        N, D, L, F = self.tokens, self.dim, self.depth, self.mlp
+        per_block = N * D * 3 * D + 2 * N * D * F + (N * D * D if N <= 256 else 0)
+        return 2 * (L - 1) * per_block / 1e9
+
 
 ARCHS: Dict[str, ViTArch] = {
     "vit_tiny_patch16_224": ViTArch("vit_tiny_patch16_224", 224, 16, 192, 12, 3, 768),

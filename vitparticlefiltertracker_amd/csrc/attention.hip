@@ -978,7 +978,10 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     // N <= 256: the key-pipelined kernel (8 waves, one strip each, the head's whole K / V image in LDS); N > 256: the
     // key-streamed, query-blocked kernel. (Round 4's persistent chunk-ring form of the N <= 256 kernel is bit-identical
     // but 1.5x slower: tools/gemm_lab/attention_lab.hip, profiles/r4_lab/attn_ring_ab_v*.txt.)
-    if (N <= 256) {
+#ifndef VPF_ATTN_STREAM_MIN_N   // LAB A/B only: route N >= this to the key-streamed kernel (product: N > 256)
+#define VPF_ATTN_STREAM_MIN_N 257
+#endif
+    if (N < VPF_ATTN_STREAM_MIN_N) {
         static bool pipe_attr = false;   // benign race: idempotent attribute set
         if (!pipe_attr) {
             (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, false>,
