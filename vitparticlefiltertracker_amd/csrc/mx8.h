@@ -39,13 +39,17 @@ __device__ __forceinline__ uint32_t mx8_amax8(uint4 v) {
 // 8 packed bf16 values -> 8 e4m3 bytes of RNE(x * 2^-E) (E = the block exponent), by gfx950's
 // v_cvt_scalef32_pk_fp8_bf16: the packed bf16 pair converted with the block scale in one instruction (4 per 8 values
 // instead of 8 unpacks + 8 multiplies + 4 v_cvt_pk_fp8_f32). The instruction divides by its scale operand: with scale
-// 2^E it is bit-identical to RNE(x * 2^-E) for every E in [-127, 125] (tools/micro/cvt_scalef.py on the MI355X: 0 of
+// 2^E it is bit-identical to RNE(x * 2^-E) for every E in [-127, 125], E = -127 included (see sc below) (tools/micro/cvt_scalef.py on the MI355X: 0 of
 // 1,048,576 pairs differ; with 2^-E 98.9 % of them differ: profiles/r4_lab/cvt_scalef_probe.txt).
 typedef __bf16 vpf_bf16x2 __attribute__((ext_vector_type(2)));
 typedef short vpf_s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint2 mx8_pack8(uint4 v, int E) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    const float sc = __uint_as_float((uint32_t)(127 + E) << 23);      // 2^E (normal for E in [-127, 125])
+    // 2^E as an fp32 bit pattern: a normal float for E in [-126, 125]. E = -127 (a block whose max is below 2^-118,
+    // e.g. all zeros) gives the bit pattern of +0.0, not 2^-127: the result is still RNE(x * 2^127) because the
+    // instruction takes only the exponent field of its scale operand (tools/micro/cvt_scalef.py covers E = -127 among
+    // its random blocks: 0 differences), which this code relies on.
+    const float sc = __uint_as_float((uint32_t)(127 + E) << 23);
     vpf_s16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(vpf_s16x2{0, 0}, __builtin_bit_cast(vpf_bf16x2, w[0]), sc,
                                                              false);
     lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(lo, __builtin_bit_cast(vpf_bf16x2, w[1]), sc, true);
