@@ -142,6 +142,14 @@ int vpf_row_stats_bf16(const uint16_t* x, int64_t rows, int D, int64_t x_stride,
 int vpf_row_stats_f32(const float* x, int64_t rows, int D, int64_t x_stride, float eps, float* out,
                       void* stream);
 
+/* H4 (folded form, from the producers' statistics planes): out[r] = {mean, rstd} of row r from parts planes
+ * fp32[parts][plane_stride][2] of {sum, sumsq} over disjoint column blocks (a vpf_gemm_bf16 stats_out), D the row
+ * length: mean = sum/D, rstd = 1/sqrt(max(sumsq/D - mean^2, 0) + eps), computed exactly as vpf_gemm_bf16's in-kernel
+ * combine (so an EPI_LN* GEMM given these {mean, rstd} with stats_parts = 0 writes the same bits as one given the
+ * planes). For consumers whose plane count exceeds what the ping-pong GEMM keeps in LDS (ViT-L: 16). */
+int vpf_stats_combine(const float* planes, int parts, int64_t plane_stride, int64_t rows, int D, float eps, float* out,
+                      void* stream);
+
 /* H4: y = LayerNorm(x) per row (fp32 statistics). Row r of x at x + r*x_stride; D % 4 == 0, D <= 1024. */
 int vpf_layernorm_bf16(const uint16_t* x, int64_t rows, int D, int64_t x_stride, const float* gamma,
                        const float* beta, float eps, uint16_t* y, int64_t y_stride, void* stream);

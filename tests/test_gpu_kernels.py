@@ -232,6 +232,29 @@ def test_gemm_stats_planes(M, D):
     torch.testing.assert_close(out.double(), ref, rtol=2e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("M,D,N,epi", [(4099, 1024, 3072, 4), (2500, 1024, 4096, 5), (777, 768, 2304, 4)])
+def test_stats_combine_equals_in_kernel_combine(M, D, N, epi):
+    """vpf_stats_combine (round 5): the producer's statistics planes combined into {mean, rstd} by a separate pass, then
+    the LN-folded GEMM with stats_parts = 0 (ViT-L's 16 planes then run the ping-pong kernel), gives the same bits as the
+    GEMM combining the planes itself (16 planes: kernel 1's wide form; 12: the ping-pong kernel's)."""
+    torch.manual_seed(M + D)
+    P = D // 64
+    h = (torch.randn(M, D, device=DEV) + 0.3).to(torch.bfloat16)
+    planes = _planes_ref(h, P).float().contiguous()
+    W = (torch.randn(N, D, device=DEV) / D ** 0.5).to(torch.bfloat16)
+    bias = 0.1 * torch.randn(N, device=DEV)
+    colsum = W.float().sum(1).contiguous()
+    ref = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    vpf().gemm(h, W, bias, None, None, 0, planes, colsum, epi, ref, P, 1e-6)
+    st = torch.empty(M, 2, device=DEV)
+    vpf().stats_combine_(planes, D, 1e-6, st)
+    got = torch.empty_like(ref)
+    vpf().gemm(h, W, bias, None, None, 0, st, colsum, epi, got)
+    assert torch.equal(got, ref)
+    mean, var = h.double().mean(1), h.double().var(1, unbiased=False)
+    torch.testing.assert_close(st.double(), torch.stack([mean, 1 / torch.sqrt(var + 1e-6)], 1), rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("M,N,K,P", [(777, 768, 768, 12), (1000, 2304, 3072, 12), (806912 // 8, 3072, 768, 12),
                                      (3001, 2304, 64, 12), (4099, 1024, 192, 16)])
 def test_gemm_kernel_variants_bit_identical(M, N, K, P):

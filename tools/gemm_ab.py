@@ -24,6 +24,11 @@ SHAPES = {  # name: (N, K, epilogue)
     "proj_bias": (768, 768, E.VPF_EPI_BIAS),
     "fc1_bias": (3072, 768, E.VPF_EPI_BIAS),
     "fc2_bias": (768, 3072, E.VPF_EPI_BIAS),
+    # ViT-L/14 @ 336 (configs[3]; run with AB_M=2363392 = 4096 x 577)
+    "qkv_l": (3072, 1024, E.VPF_EPI_LN),
+    "proj_l": (1024, 1024, E.VPF_EPI_BIAS_RESIDUAL),
+    "fc1_l": (4096, 1024, E.VPF_EPI_LN_GELU),
+    "fc2_l": (1024, 4096, E.VPF_EPI_BIAS_RESIDUAL),
 }
 
 

@@ -50,6 +50,7 @@ SIGNATURES = {
     "vpf_gemm_tune": [_I32, _I32],
     "vpf_gemm_f32": [_P, _I64, _P, _P, _P, _P, _I32, _P, _P, _P, _I64, _I64, _I64, _I64, _I32, _P],
     "vpf_row_stats_bf16": [_P, _I64, _I32, _I64, _F32, _P, _P],
+    "vpf_stats_combine": [_P, _I32, _I64, _I64, _I32, _F32, _P, _P],
     "vpf_row_stats_f32": [_P, _I64, _I32, _I64, _F32, _P, _P],
     "vpf_layernorm_bf16": [_P, _I64, _I32, _I64, _P, _P, _F32, _P, _I64, _P],
     "vpf_layernorm_f32": [_P, _I64, _I32, _I64, _P, _P, _F32, _P, _I64, _P],

@@ -237,6 +237,25 @@ int clsw_launch(const T* tokens, int64_t n, int N, int D, const float* gamma, co
     VPF_RETURN_LAUNCH();
 }
 
+// H4 for LN-folded consumers with more statistics planes than their LDS holds next to the ping-pong ring (ViT-L: 16):
+// the producer GEMMs' {sum, sumsq} planes combined into {mean, rstd} per row, one thread per row, with the same
+// operations in the same order as the consuming GEMM's in-kernel combine (gemm_bf16.hip), so the consumer's output is
+// bit-identical either way. Reads 8 B per plane and row (coalesced across the threads of a plane).
+__global__ __launch_bounds__(256) void k_stats_combine(const float2* __restrict__ planes, int parts, int64_t pstride,
+                                                       int64_t rows, float inv_k, float eps, float2* __restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    float sm = 0.f, sq = 0.f;
+    for (int p = 0; p < parts; ++p) {
+        const float2 st = planes[p * pstride + r];
+        sm += st.x;
+        sq += st.y;
+    }
+    const float mean = sm * inv_k;
+    const float var = fmaxf(fmaf(sq, inv_k, -mean * mean), 0.f);
+    out[r] = make_float2(mean, __builtin_amdgcn_rsqf(var + eps));
+}
+
 }  // namespace
 
 VPF_API int vpf_layernorm_bf16(const uint16_t* x, int64_t rows, int D, int64_t x_stride, const float* gamma,
@@ -254,6 +273,16 @@ VPF_API int vpf_row_stats_bf16(const uint16_t* x, int64_t rows, int D, int64_t x
 VPF_API int vpf_row_stats_f32(const float* x, int64_t rows, int D, int64_t x_stride, float eps, float* out,
                               void* stream) {
     return stats_launch<float>(x, rows, D, x_stride, eps, out, stream);
+}
+VPF_API int vpf_stats_combine(const float* planes, int parts, int64_t plane_stride, int64_t rows, int D, float eps,
+                              float* out, void* stream) {
+    if (!planes || !out || parts < 1 || parts > 64 || rows < 1 || plane_stride < rows || D < 1 || !(eps >= 0.f) ||
+        ((uintptr_t)planes & 7) || ((uintptr_t)out & 7) || (rows + 255) / 256 > INT32_MAX)
+        return VPF_ERR_ARG;
+    hipLaunchKernelGGL(k_stats_combine, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float2*>(planes), parts, plane_stride, rows, 1.0f / (float)D, eps,
+                       reinterpret_cast<float2*>(out));
+    VPF_RETURN_LAUNCH();
 }
 VPF_API int vpf_cls_weight_bf16(const uint16_t* tokens, int64_t n, int N, int D, const float* gamma,
                                 const float* beta, float eps, const float* tmpl, float lam, int bits,

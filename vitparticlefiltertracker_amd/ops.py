@@ -352,6 +352,19 @@ def row_stats(x: torch.Tensor, eps: float, out: torch.Tensor) -> None:
     call(name, ptr(x), rows, x.shape[1], xs, eps, ptr(out), stream_ptr())
 
 
+@torch.library.custom_op("vpf::stats_combine_", mutates_args={"out"}, device_types="cuda")
+def stats_combine_(planes: torch.Tensor, D: int, eps: float, out: torch.Tensor) -> None:
+    """H4 (folded): out[r] = (mean, rstd) of row r from the statistics planes f32[P][rows][2] (a producer GEMM's
+    stats_out view) over a row length D (vpf_stats_combine; bit-identical to the consuming GEMM's own combine)."""
+    _dev(planes, out)
+    _chk(planes.dtype == _F32 and planes.dim() == 3 and planes.shape[2] == 2 and planes.stride(2) == 1
+         and planes.stride(1) == 2, "stats_combine_: planes f32[P][rows][2]")
+    rows = planes.shape[1]
+    _chk(out.dtype == _F32 and out.is_contiguous() and out.numel() >= 2 * rows, "stats_combine_: out f32[rows][2]")
+    call("vpf_stats_combine", ptr(planes), planes.shape[0], planes.stride(0) // 2, rows, D, eps, ptr(out),
+         stream_ptr())
+
+
 @torch.library.custom_op("vpf::layernorm", mutates_args={"out"}, device_types="cuda")
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor) -> None:
     """H4: row LayerNorm over the last dim of 2-D (row-strided) views x -> out."""

@@ -329,9 +329,15 @@ class ViTEngine:
         plc = self.planes_cls_flat[: P * n * 2].view(P, n, 2)  # planes of the last block's CLS rows
 
         def ln_stats(x, st_rows, pln):
-            """LayerNorm statistics of rows x for an LN-folded GEMM: the producer's planes, or a row_stats pass."""
+            """LayerNorm statistics of rows x for an LN-folded GEMM: the producer's planes combined into {mean, rstd} by
+            one small pass (vpf_stats_combine: 8 B per plane and row), then the GEMM reads one {mean, rstd} plane. The
+            result is bit-identical to the GEMM combining the planes itself, and faster, combine included (round 5,
+            profiles/r5_lab/planes_combine_ab.txt): ViT-B QKV -1.8 %, FC1 -0.9 %; ViT-L QKV -4.0 %, FC1 -4.4 % (its 16
+            planes exceed what the ping-pong kernel holds in LDS, so QKV / FC1 also leave kernel 1's wide form).
+            Without planes (no fold or > 16 of them) a row_stats pass."""
             if planes:
-                return pln, P
+                _run(T, "stats_combine", vpf.stats_combine_, pln, D, eps, st_rows)
+                return st_rows, 0
             _run(T, "row_stats", vpf.row_stats, x, eps, st_rows)
             return st_rows, 0
 
@@ -353,9 +359,13 @@ class ViTEngine:
             hq = hq[: n * N]
 
             def ln_stats8(x):
-                """LN statistics for an MX8 consumer: the planes when it can hold them, else a row_stats pass."""
+                """LN statistics for an MX8 consumer: the planes when it can hold them (<= 13), else the planes combined
+                into {mean, rstd}, else a row_stats pass."""
                 if self.planes8:
                     return pl, P
+                if planes:
+                    _run(T, "stats_combine", vpf.stats_combine_, pl, D, eps, st)
+                    return st, 0
                 _run(T, "row_stats", vpf.row_stats, x, eps, st)
                 return st, 0
         for l, L in enumerate(self.layers):
