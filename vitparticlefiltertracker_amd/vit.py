@@ -222,8 +222,6 @@ class ViTEngine:
         if self.fp8:
             self.h8 = ops.mx8_empty(n * N, D, dev)
             self.hid8 = ops.mx8_empty(n * N, F, dev)
-        # the MX8 consumers read at most 13 statistics planes (LDS budget, vpf_gemm_mx8)
-        self.planes8 = self.use_planes and self.parts <= 13
         if self.cls_fused:
             self.clsG = torch.empty(n, A.heads * D, device=dev, dtype=dt)
             self.clsU = torch.empty(n, A.heads * D, device=dev, dtype=dt)
@@ -359,10 +357,8 @@ class ViTEngine:
             hq = hq[: n * N]
 
             def ln_stats8(x):
-                """LN statistics for an MX8 consumer: the planes when it can hold them (<= 13), else the planes combined
-                into {mean, rstd}, else a row_stats pass."""
-                if self.planes8:
-                    return pl, P
+                """LN statistics for an MX8 consumer: the planes combined into {mean, rstd} (as ln_stats: MX8 QKV -3.3 %
+                in one process, bit-identical, profiles/r5_lab/planes_combine_ab.txt), else a row_stats pass."""
                 if planes:
                     _run(T, "stats_combine", vpf.stats_combine_, pl, D, eps, st)
                     return st, 0
