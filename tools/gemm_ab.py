@@ -24,6 +24,7 @@ SHAPES = {  # name: (N, K, epilogue)
     "proj_bias": (768, 768, E.VPF_EPI_BIAS),
     "fc1_bias": (3072, 768, E.VPF_EPI_BIAS),
     "fc2_bias": (768, 3072, E.VPF_EPI_BIAS),
+    "patch": (768, 768, E.VPF_EPI_PATCH),   # ViT-B/16 patch embed (196 patch rows per crop, CLS-offset output rows)
     # ViT-L/14 @ 336 (configs[3]; run with AB_M=2363392 = 4096 x 577)
     "qkv_l": (3072, 1024, E.VPF_EPI_LN),
     "proj_l": (1024, 1024, E.VPF_EPI_BIAS_RESIDUAL),
@@ -53,13 +54,22 @@ def main():
         colsum = w.float().sum(1).contiguous()
         stats = torch.stack([torch.rand(M, device=dev, generator=g) * 0.2 - 0.1,
                              torch.rand(M, device=dev, generator=g) + 0.5], 1).contiguous()
-        res0 = (torch.rand(M, N, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+        patch = epi == E.VPF_EPI_PATCH
+        g2 = 196
+        Mp = M // g2 * g2 if patch else M
+        if patch:
+            a = a[:Mp]
+        pos = torch.rand(g2 + 1, N, device=dev, generator=g) * 0.1 if patch else None
+        res0 = (torch.rand(Mp // g2 * (g2 + 1) if patch else M, N, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
         outs = {}
         flop = 2.0 * M * N * K
         ln = epi in (E.VPF_EPI_LN, E.VPF_EPI_LN_GELU)
         resid = epi == E.VPF_EPI_BIAS_RESIDUAL
 
         def run(out):
+            if patch:
+                vpf.gemm(a, w, bias, None, pos, g2, None, None, epi, out)
+                return
             vpf.gemm(a, w, bias, out if resid else None, None, 0, stats if ln else None, colsum if ln else None,
                      epi, out)
 

@@ -41,65 +41,6 @@ __device__ __forceinline__ uint32_t rgba_tap(const uint32_t* __restrict__ rgba, 
 }
 __device__ __forceinline__ float chan(uint32_t px, int c) { return (float)((px >> (8 * c)) & 255u); }
 
-// Generic: one thread = 8 consecutive im2col columns of one row (any patch / Kp).
-template <typename OutT>
-__global__ __launch_bounds__(256) void k_crop_patches(const uint32_t* __restrict__ rgba, int H, int W,
-                                                      const float* __restrict__ xs,
-                                                      const float* __restrict__ ys,
-                                                      const float* __restrict__ ss, int64_t n_rows,
-                                                      int n_patches, int g, float w0, float h0, int S,
-                                                      int patch, int Kp, NormAB nab,
-                                                      OutT* __restrict__ out) {
-    const int chunks = Kp >> 3;
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid >= n_rows * chunks) return;
-    const int64_t row = tid / chunks;
-    const int ch = (int)(tid - row * chunks);
-    const int64_t p = row / n_patches;
-    const int pi = (int)(row - p * n_patches);
-    const int py = pi / g, px = pi - (pi / g) * g;
-    const float s = ss[p];
-    const float bw = s * w0, bh = s * h0;
-    const float x0 = xs[p] - 0.5f * bw, y0 = ys[p] - 0.5f * bh;
-    const float dx = bw / (float)S, dy = bh / (float)S;
-    const int pp = patch * patch;
-    const int K = 3 * pp;
-    float vals[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int k = ch * 8 + e;
-        float o = 0.0f;
-        if (k < K) {
-            const int c = k / pp;
-            const int r = k - c * pp;
-            const int ky = r / patch, kx = r - (r / patch) * patch;
-            const int oy = py * patch + ky, ox = px * patch + kx;
-            const float sy = (y0 + ((float)oy + 0.5f) * dy) - 0.5f;
-            const float sx = (x0 + ((float)ox + 0.5f) * dx) - 0.5f;
-            const float fy0 = floorf(sy), fx0 = floorf(sx);
-            const float fy = sy - fy0, fx = sx - fx0;
-            const int iy = (int)fy0, ix = (int)fx0;
-            const float p00 = chan(rgba_tap(rgba, H, W, iy, ix), c), p01 = chan(rgba_tap(rgba, H, W, iy, ix + 1), c);
-            const float p10 = chan(rgba_tap(rgba, H, W, iy + 1, ix), c), p11 = chan(rgba_tap(rgba, H, W, iy + 1, ix + 1), c);
-            const float top = (1.0f - fx) * p00 + fx * p01;
-            const float bot = (1.0f - fx) * p10 + fx * p11;
-            const float v = (1.0f - fy) * top + fy * bot;
-            o = fmaf(v, nab.a[c], nab.b[c]);
-        }
-        vals[e] = o;
-    }
-    OutT* dst = out + row * (int64_t)Kp + ch * 8;
-    if constexpr (sizeof(OutT) == 2) {
-        uint4 pk;
-        pk.x = pack_bf2(vals[0], vals[1]); pk.y = pack_bf2(vals[2], vals[3]);
-        pk.z = pack_bf2(vals[4], vals[5]); pk.w = pack_bf2(vals[6], vals[7]);
-        *reinterpret_cast<uint4*>(dst) = pk;
-    } else {
-        *reinterpret_cast<float4*>(dst) = make_float4(vals[0], vals[1], vals[2], vals[3]);
-        *reinterpret_cast<float4*>(dst + 4) = make_float4(vals[4], vals[5], vals[6], vals[7]);
-    }
-}
-
 // Fast path (patch % 8 == 0, Kp == 3 patch^2), LDS-staged: one 512-thread workgroup per particle; a thread writes 8
 // consecutive output pixels of one patch row (ky, kx0..kx0+7) in all three channels, the source row (sy, fy, iy)
 // computed once, each sample's column once, and one dword tap serving all three channels. The particle's source window (every The particle's source window (every
@@ -113,6 +54,49 @@ __global__ __launch_bounds__(256) void k_crop_patches(const uint32_t* __restrict
 #endif
 constexpr int CROP_LDS_DW = VPF_CROP_LDS_DW;   // 40 KiB: four workgroups per CU (0.45-0.49 vs 0.53 ms at 80 KiB and two per CU,
 // profiles/r2_gemm_lab/crop_lds_window_ab.txt); windows up to ~101 x 101 (a 64 x 64 template to scale ~1.55)
+// The particle's crop geometry and its source window (every bilinear tap of its S x S samples, clamped into the zero
+// border as rgba_tap does), staged into LDS when it fits; shared by both LDS kernels.
+struct CropWin {
+    float x0, y0, dx, dy;
+    int cx0, cy0, wx;
+    bool staged;
+};
+template <int NT>
+__device__ __forceinline__ CropWin stage_window(uint32_t* win, const uint32_t* __restrict__ rgba, int H, int W, float xc,
+                                                float yc, float sc, float w0, float h0, int S) {
+    CropWin cw;
+    const float bw = sc * w0, bh = sc * h0;
+    cw.x0 = xc - 0.5f * bw;
+    cw.y0 = yc - 0.5f * bh;
+    cw.dx = bw / (float)S;
+    cw.dy = bh / (float)S;
+    // tap range: the sample coordinate is monotone in the output index, so the first and last samples bound it
+    const int ix_lo = (int)floorf((cw.x0 + (0.0f + 0.5f) * cw.dx) - 0.5f);
+    const int ix_hi = (int)floorf((cw.x0 + ((float)(S - 1) + 0.5f) * cw.dx) - 0.5f) + 1;
+    const int iy_lo = (int)floorf((cw.y0 + (0.0f + 0.5f) * cw.dy) - 0.5f);
+    const int iy_hi = (int)floorf((cw.y0 + ((float)(S - 1) + 0.5f) * cw.dy) - 0.5f) + 1;
+    cw.cx0 = min(max(ix_lo, -1), W);
+    const int cx1 = min(max(ix_hi, -1), W);
+    cw.cy0 = min(max(iy_lo, -1), H);
+    const int cy1 = min(max(iy_hi, -1), H);
+    cw.wx = cx1 - cw.cx0 + 1;
+    const int wy = cy1 - cw.cy0 + 1;
+    cw.staged = cw.wx * wy <= CROP_LDS_DW;   // workgroup-uniform
+    if (cw.staged) {
+        for (int i = threadIdx.x; i < cw.wx * wy; i += NT) {
+            const int r = i / cw.wx, c = i - r * cw.wx;
+            win[i] = rgba[(int64_t)(cw.cy0 + r + 1) * (W + 2) + (cw.cx0 + c + 1)];
+        }
+    }
+    __syncthreads();
+    return cw;
+}
+__device__ __forceinline__ uint32_t win_tap(const CropWin& cw, const uint32_t* win, const uint32_t* __restrict__ rgba,
+                                            int H, int W, int yy, int xx) {
+    if (cw.staged) return win[(min(max(yy, -1), H) - cw.cy0) * cw.wx + (min(max(xx, -1), W) - cw.cx0)];
+    return rgba_tap(rgba, H, W, yy, xx);
+}
+
 template <typename OutT>
 __global__ __launch_bounds__(512) void k_crop_patches_lds(const uint32_t* __restrict__ rgba, int H, int W,
                                                           const float* __restrict__ xs, const float* __restrict__ ys,
@@ -121,30 +105,9 @@ __global__ __launch_bounds__(512) void k_crop_patches_lds(const uint32_t* __rest
                                                           OutT* __restrict__ out) {
     __shared__ uint32_t win[CROP_LDS_DW];
     const int64_t p = blockIdx.x;
-    const float s = ss[p];
-    const float bw = s * w0, bh = s * h0;
-    const float x0 = xs[p] - 0.5f * bw, y0 = ys[p] - 0.5f * bh;
-    const float dx = bw / (float)S, dy = bh / (float)S;
-    // tap range: the sample coordinate is monotone in the output index, so the first and last samples bound it
-    const int ix_lo = (int)floorf((x0 + (0.0f + 0.5f) * dx) - 0.5f);
-    const int ix_hi = (int)floorf((x0 + ((float)(S - 1) + 0.5f) * dx) - 0.5f) + 1;
-    const int iy_lo = (int)floorf((y0 + (0.0f + 0.5f) * dy) - 0.5f);
-    const int iy_hi = (int)floorf((y0 + ((float)(S - 1) + 0.5f) * dy) - 0.5f) + 1;
-    const int cx0 = min(max(ix_lo, -1), W), cx1 = min(max(ix_hi, -1), W);
-    const int cy0 = min(max(iy_lo, -1), H), cy1 = min(max(iy_hi, -1), H);
-    const int wx = cx1 - cx0 + 1, wy = cy1 - cy0 + 1;
-    const bool staged = wx * wy <= CROP_LDS_DW;   // workgroup-uniform
-    if (staged) {
-        for (int i = threadIdx.x; i < wx * wy; i += 512) {
-            const int r = i / wx, c = i - r * wx;
-            win[i] = rgba[(int64_t)(cy0 + r + 1) * (W + 2) + (cx0 + c + 1)];
-        }
-    }
-    __syncthreads();
-    auto tap = [&](int yy, int xx) -> uint32_t {
-        if (staged) return win[(min(max(yy, -1), H) - cy0) * wx + (min(max(xx, -1), W) - cx0)];
-        return rgba_tap(rgba, H, W, yy, xx);
-    };
+    const CropWin cw = stage_window<512>(win, rgba, H, W, xs[p], ys[p], ss[p], w0, h0, S);
+    const float x0 = cw.x0, y0 = cw.y0, dx = cw.dx, dy = cw.dy;
+    auto tap = [&](int yy, int xx) -> uint32_t { return win_tap(cw, win, rgba, H, W, yy, xx); };
     const int per_row = patch * (patch >> 3);             // threads per im2col row
     const int pp = patch * patch;
     for (int t = threadIdx.x; t < n_patches * per_row; t += 512) {
@@ -192,6 +155,66 @@ __global__ __launch_bounds__(512) void k_crop_patches_lds(const uint32_t* __rest
     }
 }
 
+// Any patch / Kp (ViT-L/14: patch 14, Kp = 640 > 3 x 196), LDS-staged like the fast path: one 512-thread workgroup
+// per particle stages its source window, then a thread writes 8 consecutive im2col columns of one row (per element:
+// channel, tap and weights from the column index; columns past 3 patch^2 are the zero padding). Same per-value
+// arithmetic (and order) as the oracle. Round 5: replaces a global-tap form (4.8 ms per ViT-L frame) whose 32 gathered
+// dword taps per thread went through the vector memory path.
+template <typename OutT>
+__global__ __launch_bounds__(512) void k_crop_patches_gen(const uint32_t* __restrict__ rgba, int H, int W,
+                                                          const float* __restrict__ xs, const float* __restrict__ ys,
+                                                          const float* __restrict__ ss, int n_patches, int g, float w0,
+                                                          float h0, int S, int patch, int Kp, NormAB nab,
+                                                          OutT* __restrict__ out) {
+    __shared__ uint32_t win[CROP_LDS_DW];
+    const int64_t p = blockIdx.x;
+    const CropWin cw = stage_window<512>(win, rgba, H, W, xs[p], ys[p], ss[p], w0, h0, S);
+    const int chunks = Kp >> 3;
+    const int pp = patch * patch;
+    const int K = 3 * pp;
+    for (int t = threadIdx.x; t < n_patches * chunks; t += 512) {
+        const int pi = t / chunks;
+        const int ch = t - pi * chunks;
+        const int py = pi / g, px = pi - (pi / g) * g;
+        float vals[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = ch * 8 + e;
+            float o = 0.0f;
+            if (k < K) {
+                const int c = k / pp;
+                const int r = k - c * pp;
+                const int ky = r / patch, kx = r - (r / patch) * patch;
+                const int oy = py * patch + ky, ox = px * patch + kx;
+                const float sy = (cw.y0 + ((float)oy + 0.5f) * cw.dy) - 0.5f;
+                const float sx = (cw.x0 + ((float)ox + 0.5f) * cw.dx) - 0.5f;
+                const float fy0 = floorf(sy), fx0 = floorf(sx);
+                const float fy = sy - fy0, fx = sx - fx0;
+                const int iy = (int)fy0, ix = (int)fx0;
+                const float p00 = chan(win_tap(cw, win, rgba, H, W, iy, ix), c);
+                const float p01 = chan(win_tap(cw, win, rgba, H, W, iy, ix + 1), c);
+                const float p10 = chan(win_tap(cw, win, rgba, H, W, iy + 1, ix), c);
+                const float p11 = chan(win_tap(cw, win, rgba, H, W, iy + 1, ix + 1), c);
+                const float top = (1.0f - fx) * p00 + fx * p01;
+                const float bot = (1.0f - fx) * p10 + fx * p11;
+                const float v = (1.0f - fy) * top + fy * bot;
+                o = fmaf(v, nab.a[c], nab.b[c]);
+            }
+            vals[e] = o;
+        }
+        OutT* dst = out + (p * n_patches + pi) * (int64_t)Kp + ch * 8;
+        if constexpr (sizeof(OutT) == 2) {
+            uint4 pk;
+            pk.x = pack_bf2(vals[0], vals[1]); pk.y = pack_bf2(vals[2], vals[3]);
+            pk.z = pack_bf2(vals[4], vals[5]); pk.w = pack_bf2(vals[6], vals[7]);
+            *reinterpret_cast<uint4*>(dst) = pk;
+        } else {
+            *reinterpret_cast<float4*>(dst) = make_float4(vals[0], vals[1], vals[2], vals[3]);
+            *reinterpret_cast<float4*>(dst + 4) = make_float4(vals[4], vals[5], vals[6], vals[7]);
+        }
+    }
+}
+
 template <typename OutT>
 static int crop_launch(const uint8_t* frame, int H, int W, uint32_t* rgba_ws, const float* particles, int64_t ld,
                        int64_t n, float w0, float h0, int S, int patch, int Kp, const float* norm_ab_host, OutT* out,
@@ -207,15 +230,14 @@ static int crop_launch(const uint8_t* frame, int H, int W, uint32_t* rgba_ws, co
     const int64_t npix = (int64_t)(H + 2) * (W + 2);
     hipLaunchKernelGGL(k_frame_rgba, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, frame, H, W, rgba_ws);
     const int g = S / patch;
-    const int64_t rows = n * g * g;
     if (patch % 8 == 0 && Kp == 3 * patch * patch && n <= INT32_MAX) {
         hipLaunchKernelGGL(k_crop_patches_lds<OutT>, dim3((unsigned)n), dim3(512), 0, st, rgba_ws, H, W, particles,
                            particles + ld, particles + 2 * ld, g * g, g, w0, h0, S, patch, nab, out);
+    } else if (n <= INT32_MAX) {
+        hipLaunchKernelGGL(k_crop_patches_gen<OutT>, dim3((unsigned)n), dim3(512), 0, st, rgba_ws, H, W, particles,
+                           particles + ld, particles + 2 * ld, g * g, g, w0, h0, S, patch, Kp, nab, out);
     } else {
-        const int64_t work = rows * (Kp / 8);
-        hipLaunchKernelGGL(k_crop_patches<OutT>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, rgba_ws, H, W,
-                           particles, particles + ld, particles + 2 * ld, rows, g * g, g, w0, h0, S, patch, Kp, nab,
-                           out);
+        return VPF_ERR_ARG;
     }
     VPF_RETURN_LAUNCH();
 }
