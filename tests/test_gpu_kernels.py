@@ -47,10 +47,12 @@ def test_predict_bit_exact(n, begin):
 
 # ------------------------------------------------------------------ H2/H3 crop
 @pytest.mark.parametrize("box", [(64.0, 48.0), (300.0, 200.0)])
-@pytest.mark.parametrize("S,patch,H,W", [(224, 16, 224, 224), (336, 14, 240, 320), (224, 16, 1080, 1920)])
+@pytest.mark.parametrize("S,patch,H,W", [(224, 16, 224, 224), (336, 14, 240, 320), (224, 16, 1080, 1920),
+                                         (98, 7, 100, 130), (120, 12, 200, 150)])
 def test_crop_bit_exact(S, patch, H, W, box):
     """Bit-exact against the oracle. patch 16 takes the LDS-staged kernel (one workgroup per particle, its source
-    window in LDS); the (300, 200) box at scale 2 overflows the LDS window and takes its global-tap branch."""
+    window in LDS); the (300, 200) box at scale 2 overflows the LDS window and takes its global-tap branch. Patches 14
+    and 12 (even, not a multiple of 8: bf16 pair stores) and 7 (odd: element stores) take the per-row kernel."""
     rng = np.random.default_rng(S + H)
     frame = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
     n = 5

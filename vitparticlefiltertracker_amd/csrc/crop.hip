@@ -43,7 +43,7 @@ __device__ __forceinline__ float chan(uint32_t px, int c) { return (float)((px >
 
 // Fast path (patch % 8 == 0, Kp == 3 patch^2), LDS-staged: one 512-thread workgroup per particle; a thread writes 8
 // consecutive output pixels of one patch row (ky, kx0..kx0+7) in all three channels, the source row (sy, fy, iy)
-// computed once, each sample's column once, and one dword tap serving all three channels. The particle's source window (every The particle's source window (every
+// computed once, each sample's column once, and one dword tap serving all three channels. The particle's source window (every
 // bilinear tap of its S x S samples, clamped into the zero border as rgba_tap does) is copied from the RGBA workspace
 // into LDS once, and the taps read LDS instead of issuing 32 gathered dword loads per thread through the vector
 // memory path, which bound the global form (the im2col stores are the same). A window larger than CROP_LDS_DW dwords
@@ -156,10 +156,11 @@ __global__ __launch_bounds__(512) void k_crop_patches_lds(const uint32_t* __rest
 }
 
 // Any patch / Kp (ViT-L/14: patch 14, Kp = 640 > 3 x 196), LDS-staged like the fast path: one 512-thread workgroup
-// per particle stages its source window, then a thread writes 8 consecutive im2col columns of one row (per element:
-// channel, tap and weights from the column index; columns past 3 patch^2 are the zero padding). Same per-value
-// arithmetic (and order) as the oracle. Round 5: replaces a global-tap form (4.8 ms per ViT-L frame) whose 32 gathered
-// dword taps per thread went through the vector memory path.
+// per particle stages its source window, then a thread walks one patch row (ky) of one patch: each sample's source row
+// and column are computed once and one dword tap serves all three channels; bf16 pairs go out as dword stores (even
+// patch). The columns past 3 patch^2 are the zero padding. Same per-value arithmetic (and order) as the oracle.
+// Round 5: replaces a global-tap form (4.8 ms per ViT-L frame) and a per-element form (4.35 ms) whose index and tap
+// work was repeated for every channel.
 template <typename OutT>
 __global__ __launch_bounds__(512) void k_crop_patches_gen(const uint32_t* __restrict__ rgba, int H, int W,
                                                           const float* __restrict__ xs, const float* __restrict__ ys,
@@ -169,49 +170,59 @@ __global__ __launch_bounds__(512) void k_crop_patches_gen(const uint32_t* __rest
     __shared__ uint32_t win[CROP_LDS_DW];
     const int64_t p = blockIdx.x;
     const CropWin cw = stage_window<512>(win, rgba, H, W, xs[p], ys[p], ss[p], w0, h0, S);
-    const int chunks = Kp >> 3;
-    const int pp = patch * patch;
-    const int K = 3 * pp;
-    for (int t = threadIdx.x; t < n_patches * chunks; t += 512) {
-        const int pi = t / chunks;
-        const int ch = t - pi * chunks;
-        const int py = pi / g, px = pi - (pi / g) * g;
-        float vals[8];
+    auto tap = [&](int yy, int xx) -> uint32_t { return win_tap(cw, win, rgba, H, W, yy, xx); };
+    const int pp = patch * patch, K = 3 * pp;
+    OutT* const base = out + p * n_patches * (int64_t)Kp;
+    const bool pairs = sizeof(OutT) == 2 && (patch & 1) == 0;   // 4-B aligned bf16 pairs
+    for (int t = threadIdx.x; t < n_patches * patch; t += 512) {
+        const int pi = t / patch, ky = t - pi * patch;
+        const int py = pi / g, px = pi - py * g;
+        const float sy = (cw.y0 + ((float)(py * patch + ky) + 0.5f) * cw.dy) - 0.5f;
+        const float fy0 = floorf(sy);
+        const float fy = sy - fy0;
+        const int iy = (int)fy0;
+        OutT* const row = base + (int64_t)pi * Kp + ky * patch;
+        for (int kx = 0; kx < patch; kx += 2) {
+            float v[3][2];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int k = ch * 8 + e;
-            float o = 0.0f;
-            if (k < K) {
-                const int c = k / pp;
-                const int r = k - c * pp;
-                const int ky = r / patch, kx = r - (r / patch) * patch;
-                const int oy = py * patch + ky, ox = px * patch + kx;
-                const float sy = (cw.y0 + ((float)oy + 0.5f) * cw.dy) - 0.5f;
+            for (int e = 0; e < 2; ++e) {
+                const int ox = px * patch + min(kx + e, patch - 1);   // odd patch: the last pair repeats a column
                 const float sx = (cw.x0 + ((float)ox + 0.5f) * cw.dx) - 0.5f;
-                const float fy0 = floorf(sy), fx0 = floorf(sx);
-                const float fy = sy - fy0, fx = sx - fx0;
-                const int iy = (int)fy0, ix = (int)fx0;
-                const float p00 = chan(win_tap(cw, win, rgba, H, W, iy, ix), c);
-                const float p01 = chan(win_tap(cw, win, rgba, H, W, iy, ix + 1), c);
-                const float p10 = chan(win_tap(cw, win, rgba, H, W, iy + 1, ix), c);
-                const float p11 = chan(win_tap(cw, win, rgba, H, W, iy + 1, ix + 1), c);
-                const float top = (1.0f - fx) * p00 + fx * p01;
-                const float bot = (1.0f - fx) * p10 + fx * p11;
-                const float v = (1.0f - fy) * top + fy * bot;
-                o = fmaf(v, nab.a[c], nab.b[c]);
+                const float fx0 = floorf(sx);
+                const float fx = sx - fx0;
+                const int ix = (int)fx0;
+                const uint32_t t00 = tap(iy, ix), t01 = tap(iy, ix + 1);
+                const uint32_t t10 = tap(iy + 1, ix), t11 = tap(iy + 1, ix + 1);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float top = (1.0f - fx) * chan(t00, c) + fx * chan(t01, c);
+                    const float bot = (1.0f - fx) * chan(t10, c) + fx * chan(t11, c);
+                    const float vv = (1.0f - fy) * top + fy * bot;
+                    v[c][e] = fmaf(vv, nab.a[c], nab.b[c]);
+                }
             }
-            vals[e] = o;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                OutT* dst = row + c * pp + kx;
+                if constexpr (sizeof(OutT) == 2) {
+                    const uint32_t pk = pack_bf2(v[c][0], v[c][1]);
+                    if (pairs) {
+                        *reinterpret_cast<uint32_t*>(dst) = pk;
+                    } else {
+                        dst[0] = (OutT)(pk & 0xffffu);
+                        if (kx + 1 < patch) dst[1] = (OutT)(pk >> 16);
+                    }
+                } else {
+                    dst[0] = v[c][0];
+                    if (kx + 1 < patch) dst[1] = v[c][1];
+                }
+            }
         }
-        OutT* dst = out + (p * n_patches + pi) * (int64_t)Kp + ch * 8;
-        if constexpr (sizeof(OutT) == 2) {
-            uint4 pk;
-            pk.x = pack_bf2(vals[0], vals[1]); pk.y = pack_bf2(vals[2], vals[3]);
-            pk.z = pack_bf2(vals[4], vals[5]); pk.w = pack_bf2(vals[6], vals[7]);
-            *reinterpret_cast<uint4*>(dst) = pk;
-        } else {
-            *reinterpret_cast<float4*>(dst) = make_float4(vals[0], vals[1], vals[2], vals[3]);
-            *reinterpret_cast<float4*>(dst + 4) = make_float4(vals[4], vals[5], vals[6], vals[7]);
-        }
+    }
+    const int pad = Kp - K;
+    for (int t = threadIdx.x; t < n_patches * pad; t += 512) {
+        const int pi = t / pad;
+        base[(int64_t)pi * Kp + K + (t - pi * pad)] = (OutT)0;
     }
 }
 
