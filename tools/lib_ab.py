@@ -3,7 +3,7 @@ libvpf.so (bound by vitparticlefiltertracker_amd._lib) and another build loaded 
 the lab build, tools/gemm_lab -> libvpf_lab.so, whose MX8 GEMM / attention are the round-3 snapshots). Both get the
 same device buffers; interleaved rounds, HIP-event medians, outputs compared bit for bit.
 
-Cases: bf16_qkv / bf16_proj / bf16_fc1 / bf16_fc2 (vpf_gemm_bf16 with the encoder's epilogues), mx8_fc1 (LN + GELU, MX8-only output: FC2's A operand), mx8_fc2 (residual + planes + the MX8 copy of h),
+Cases: bf16_qkv / bf16_proj / bf16_fc1 / bf16_fc2 (vpf_gemm_bf16 with the encoder's epilogues), mx8_fc1 (LN + GELU, MX8-only output: FC2's A operand), mx8_fc2 / mx8_proj (residual + planes + the MX8 copy of h),
 mx8_qkv (LN fold, bf16 out), quant (vpf_quantize_mx8 of a bf16 [M][768] tensor), attn (bf16 attention, N = 197),
 attn577 (bf16 attention at ViT-L/14 @ 336's N = 577, 16 heads).
 
@@ -89,7 +89,7 @@ def main():
                                        st)
             flop = 2.0 * M * N * K
         else:
-            N, K = {"mx8_fc1": (3072, 768), "mx8_fc2": (768, 3072), "mx8_qkv": (2304, 768)}[case]
+            N, K = {"mx8_fc1": (3072, 768), "mx8_fc2": (768, 3072), "mx8_qkv": (2304, 768), "mx8_proj": (768, 768)}[case]
             a = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
             w = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16)
             a8, as8 = ops.mx8_empty(M, K, dev)
@@ -98,19 +98,20 @@ def main():
             V.quantize_mx8_(w, 1, w8, ws8)
             bias = torch.rand(N, device=dev, generator=g) * 0.1
             colsum = w.float().sum(1).contiguous()
-            Pn = K // 64
-            planes = torch.rand(Pn, M, 2, device=dev, generator=g) + 0.5
+            Pn = 0                                     # the product's LN form: one combined {mean, rstd} plane
+            planes = torch.rand(M, 2, device=dev, generator=g) + 0.5
             res0 = (torch.rand(M, N, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
             bufs = {}
             for k in ("product", "other"):
-                out = res0.clone() if case == "mx8_fc2" else torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+                out = res0.clone() if case in ("mx8_fc2", "mx8_proj") else torch.empty(M, N, device=dev, dtype=torch.bfloat16)
                 q8, s8 = ops.mx8_empty(M, N, dev)
                 bufs[k] = (out, q8, s8, torch.empty((N + 63) // 64, M, 2, device=dev))
-            epi = {"mx8_fc1": E.VPF_EPI_LN_GELU, "mx8_fc2": E.VPF_EPI_BIAS_RESIDUAL, "mx8_qkv": E.VPF_EPI_LN}[case]
+            epi = {"mx8_fc1": E.VPF_EPI_LN_GELU, "mx8_fc2": E.VPF_EPI_BIAS_RESIDUAL, "mx8_qkv": E.VPF_EPI_LN,
+                   "mx8_proj": E.VPF_EPI_BIAS_RESIDUAL}[case]
 
             def call(L, k, reset=False):
                 out, q8, s8, pl = bufs[k]
-                fc1, fc2 = case == "mx8_fc1", case == "mx8_fc2"
+                fc1, fc2 = case == "mx8_fc1", case in ("mx8_fc2", "mx8_proj")
                 if fc2 and reset:                      # the residual is read in place: same input for the bit check
                     out.copy_(res0)
                 return L.vpf_gemm_mx8(pt(a8), a8.stride(0), pt(as8), as8.shape[1], pt(w8), pt(ws8), pt(bias),
