@@ -1,5 +1,6 @@
-"""Design aid: libvpf attention kernels (VPF_ATTN_MODE 0 = whole-image per-(particle, head) workgroups, 2 = key-pipelined (default for N <= 256)
-double-buffered) on the ViT-B/16 shape at 4096 particles, interleaved rounds in one process."""
+"""Design aid (round 1): attention kernels (VPF_ATTN_MODE 0 = whole-image per-(particle, head) workgroups, 2 = key-pipelined
+double-buffered) on the ViT-B/16 shape at 4096 particles, interleaved rounds in one process. The modes are read only by
+the lab build (tools/gemm_lab -> libvpf_lab.so, loaded with VPF_LIB_PATH); the product library has no mode switch."""
 import os, sys
 import torch
 sys.path.insert(0, ".")

@@ -43,7 +43,7 @@ def main():
         outs = {}
         if case in ("attn", "attn577"):
             # attn: ViT-B/16 @ 224 (N = 197, 12 heads, the key-pipelined kernel); attn577: ViT-L/14 @ 336 (N = 577,
-            # 16 heads, the whole-image kernel), 4096 particles unless AB_M says otherwise
+            # 16 heads, the key-streamed kernel), 4096 particles unless AB_M says otherwise
             N, H = (197, 12) if case == "attn" else (577, 16)
             B = M // 197
             qkv = (torch.randn(B, N, 3 * 64 * H, device=dev, generator=g) * 1.5).to(torch.bfloat16)
