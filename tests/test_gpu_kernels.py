@@ -234,7 +234,8 @@ def test_gemm_stats_planes(M, D):
     torch.testing.assert_close(out.double(), ref, rtol=2e-2, atol=3e-2)
 
 
-@pytest.mark.parametrize("M,D,N,epi", [(4099, 1024, 3072, 4), (2500, 1024, 4096, 5), (777, 768, 2304, 4)])
+@pytest.mark.parametrize("M,D,N,epi", [(4099, 1024, 3072, 4), (2500, 1024, 4096, 5), (777, 768, 2304, 4),
+                                         (1, 192, 576, 4), (257, 192, 768, 5)])
 def test_stats_combine_equals_in_kernel_combine(M, D, N, epi):
     """vpf_stats_combine (round 5): the producer's statistics planes combined into {mean, rstd} by a separate pass, then
     the LN-folded GEMM with stats_parts = 0 (ViT-L's 16 planes then run the ping-pong kernel), gives the same bits as the
