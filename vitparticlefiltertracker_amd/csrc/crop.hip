@@ -102,15 +102,20 @@ __global__ __launch_bounds__(512) void k_crop_patches_lds(const uint32_t* __rest
                                                           const float* __restrict__ xs, const float* __restrict__ ys,
                                                           const float* __restrict__ ss, int n_patches, int g, float w0,
                                                           float h0, int S, int patch, NormAB nab,
-                                                          OutT* __restrict__ out) {
+                                                          OutT* __restrict__ out, int split) {
     __shared__ uint32_t win[CROP_LDS_DW];
-    const int64_t p = blockIdx.x;
+    // `split` workgroups per particle (small batches: the 8-GPU share's 512 particles would fill 2 workgroups per CU),
+    // each staging the window and writing a contiguous share of the particle's rows
+    const int64_t p = blockIdx.x / split;
+    const int part = blockIdx.x - (int)(p * split);
     const CropWin cw = stage_window<512>(win, rgba, H, W, xs[p], ys[p], ss[p], w0, h0, S);
     const float x0 = cw.x0, y0 = cw.y0, dx = cw.dx, dy = cw.dy;
     auto tap = [&](int yy, int xx) -> uint32_t { return win_tap(cw, win, rgba, H, W, yy, xx); };
     const int per_row = patch * (patch >> 3);             // threads per im2col row
     const int pp = patch * patch;
-    for (int t = threadIdx.x; t < n_patches * per_row; t += 512) {
+    const int total = n_patches * per_row;
+    const int t_end = (int)((int64_t)total * (part + 1) / split);
+    for (int t = (int)((int64_t)total * part / split) + threadIdx.x; t < t_end; t += 512) {
         const int pi = t / per_row;
         const int tt = t - pi * per_row;
         const int ky = tt / (patch >> 3), kx0 = (tt - ky * (patch >> 3)) * 8;
@@ -241,9 +246,10 @@ static int crop_launch(const uint8_t* frame, int H, int W, uint32_t* rgba_ws, co
     const int64_t npix = (int64_t)(H + 2) * (W + 2);
     hipLaunchKernelGGL(k_frame_rgba, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, frame, H, W, rgba_ws);
     const int g = S / patch;
-    if (patch % 8 == 0 && Kp == 3 * patch * patch && n <= INT32_MAX) {
-        hipLaunchKernelGGL(k_crop_patches_lds<OutT>, dim3((unsigned)n), dim3(512), 0, st, rgba_ws, H, W, particles,
-                           particles + ld, particles + 2 * ld, g * g, g, w0, h0, S, patch, nab, out);
+    if (patch % 8 == 0 && Kp == 3 * patch * patch && n <= INT32_MAX / 4) {
+        const int split = n >= 2048 ? 1 : n >= 1024 ? 2 : 4;   // at least ~4096 workgroups when the batch is small
+        hipLaunchKernelGGL(k_crop_patches_lds<OutT>, dim3((unsigned)(n * split)), dim3(512), 0, st, rgba_ws, H, W,
+                           particles, particles + ld, particles + 2 * ld, g * g, g, w0, h0, S, patch, nab, out, split);
     } else if (n <= INT32_MAX) {
         hipLaunchKernelGGL(k_crop_patches_gen<OutT>, dim3((unsigned)n), dim3(512), 0, st, rgba_ws, H, W, particles,
                            particles + ld, particles + 2 * ld, g * g, g, w0, h0, S, patch, Kp, nab, out);

@@ -241,15 +241,29 @@ int clsw_launch(const T* tokens, int64_t n, int N, int D, const float* gamma, co
 // the producer GEMMs' {sum, sumsq} planes combined into {mean, rstd} per row, one thread per row, with the same
 // operations in the same order as the consuming GEMM's in-kernel combine (gemm_bf16.hip), so the consumer's output is
 // bit-identical either way. Reads 8 B per plane and row (coalesced across the threads of a plane).
+// PARTS > 0: the plane count of the encoders (3 / 12 / 16) as a constant, so all of a row's plane loads are in flight
+// at once; the sums still run in plane order (the bits of the GEMMs' in-kernel combine). 0: any count.
+template <int PARTS>
 __global__ __launch_bounds__(256) void k_stats_combine(const float2* __restrict__ planes, int parts, int64_t pstride,
                                                        int64_t rows, float inv_k, float eps, float2* __restrict__ out) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= rows) return;
     float sm = 0.f, sq = 0.f;
-    for (int p = 0; p < parts; ++p) {
-        const float2 st = planes[p * pstride + r];
-        sm += st.x;
-        sq += st.y;
+    if constexpr (PARTS > 0) {
+        float2 st[PARTS];
+#pragma unroll
+        for (int p = 0; p < PARTS; ++p) st[p] = planes[p * pstride + r];
+#pragma unroll
+        for (int p = 0; p < PARTS; ++p) {
+            sm += st[p].x;
+            sq += st[p].y;
+        }
+    } else {
+        for (int p = 0; p < parts; ++p) {
+            const float2 st = planes[p * pstride + r];
+            sm += st.x;
+            sq += st.y;
+        }
     }
     const float mean = sm * inv_k;
     const float var = fmaxf(fmaf(sq, inv_k, -mean * mean), 0.f);
@@ -279,9 +293,19 @@ VPF_API int vpf_stats_combine(const float* planes, int parts, int64_t plane_stri
     if (!planes || !out || parts < 1 || parts > 64 || rows < 1 || plane_stride < rows || D < 1 || !(eps >= 0.f) ||
         ((uintptr_t)planes & 7) || ((uintptr_t)out & 7) || (rows + 255) / 256 > INT32_MAX)
         return VPF_ERR_ARG;
-    hipLaunchKernelGGL(k_stats_combine, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const float2*>(planes), parts, plane_stride, rows, 1.0f / (float)D, eps,
-                       reinterpret_cast<float2*>(out));
+    const dim3 grid((unsigned)((rows + 255) / 256)), block(256);
+    const float2* pl = reinterpret_cast<const float2*>(planes);
+    float2* o = reinterpret_cast<float2*>(out);
+    hipStream_t s = (hipStream_t)stream;
+    const float inv_k = 1.0f / (float)D;
+#define VPF_COMBINE(P) hipLaunchKernelGGL(k_stats_combine<P>, grid, block, 0, s, pl, parts, plane_stride, rows, inv_k, eps, o)
+    switch (parts) {
+        case 3: VPF_COMBINE(3); break;
+        case 12: VPF_COMBINE(12); break;
+        case 16: VPF_COMBINE(16); break;
+        default: VPF_COMBINE(0); break;
+    }
+#undef VPF_COMBINE
     VPF_RETURN_LAUNCH();
 }
 VPF_API int vpf_cls_weight_bf16(const uint16_t* tokens, int64_t n, int N, int D, const float* gamma,
