@@ -250,6 +250,46 @@ __device__ __forceinline__ void pv32(const char* Vt, int lane, const bf16x8 pf[2
         }
 }
 
+// pv32 split in two (VPF_ATTN_VEARLY: bit 1 the attn_step_lf steps, bit 2 attn_step_pl): the V^T fragment reads, issued right after a step's QK^T MFMAs so their latency
+// hides under the softmax, and the MFMAs behind the wait that retires them. The reads are inline asm like pv32's: the
+// builtin form made hipcc drain vmcnt(0) (every K / V DMA group in flight) before the first of them. The same reads
+// and MFMAs in the same order as pv32: bit-identical.
+#ifndef VPF_ATTN_VEARLY
+#define VPF_ATTN_VEARLY 1   // product: the N > 256 kernel's steps (-1 % at N = 577, r5_lab/attn_vearly_ab.txt)
+#endif
+template <int HALVES>
+__device__ __forceinline__ void pv_reads(const char* Vt, int lane, bf16x4 (&vr)[2][2][2]) {
+    const int grp = lane >> 4, gi = lane & 15;
+    const int rq = gi >> 2, cp = gi & 3;
+    const int rbase = 4 * (grp >> 1) + rq;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
+        const uint32_t a = (uint32_t)(size_t)Vt + (uint32_t)(v_off(rbase, col >> 3) + (col & 7) * 2);
+        vr[0][dt][0] = ds_read_tr_asm_o<0>(a);
+        vr[0][dt][1] = ds_read_tr_asm_o<1024>(a);
+        if constexpr (HALVES == 2) {
+            vr[1][dt][0] = ds_read_tr_asm_o<2048>(a);
+            vr[1][dt][1] = ds_read_tr_asm_o<3072>(a);
+        }
+    }
+}
+template <int HALVES>
+__device__ __forceinline__ void pv_mfmas(bf16x4 (&vr)[2][2][2], const bf16x8 pf[2], f32x16& o0, f32x16& o1) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1]),
+                 "+v"(vr[1][0][0]), "+v"(vr[1][0][1]), "+v"(vr[1][1][0]), "+v"(vr[1][1][1])::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int st = 0; st < HALVES; ++st)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const bf16x4 lo = vr[st][dt][0], hi = vr[st][dt][1];
+            const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o0, 0, 0, 0);
+            else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o1, 0, 0, 0);
+        }
+}
+
 // The same step in the rounds 1-4 form (the N <= 256 kernel's): the row max of every tile (T13 lazy rescale when it
 // moved by more than 2^8), l summed from the fp32 probabilities. Bit-identical to the rounds 1-4 attn_step.
 template <bool MASK>
@@ -257,6 +297,10 @@ __device__ __forceinline__ void attn_step_pl(const char* Kt, const char* Vt, int
                                              float scale_log2, float& m, float& l, f32x16& o0, f32x16& o1) {
     const int hh = lane >> 5;
     f32x16 s = qk32(Kt, lane, qf);
+#if VPF_ATTN_VEARLY & 2
+    bf16x4 vr[2][2][2];
+    pv_reads<2>(Vt, lane, vr);
+#endif
     float bm = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -286,7 +330,11 @@ __device__ __forceinline__ void attn_step_pl(const char* Kt, const char* Vt, int
     for (int st = 0; st < 2; ++st)
         pf[st] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(s[8 * st + 0], s[8 * st + 1]), pack_bf2(s[8 * st + 2], s[8 * st + 3]),
                                                        pack_bf2(s[8 * st + 4], s[8 * st + 5]), pack_bf2(s[8 * st + 6], s[8 * st + 7])));
+#if VPF_ATTN_VEARLY & 2
+    pv_mfmas<2>(vr, pf, o0, o1);
+#else
     pv32<2>(Vt, lane, pf, o0, o1);
+#endif
 }
 
 // attn_step_tail8 of rounds 1-4 (at most 8 real keys in the tile: s[0..3] only, the first 16-key PV half)
@@ -343,6 +391,10 @@ __device__ __forceinline__ void attn_step_lf(const char* Kt, const char* Vt, int
         }
     };
     f32x16 s = qk32(Kt, lane, qf);
+#if VPF_ATTN_VEARLY & 1
+    bf16x4 vr[2][2][2];
+    pv_reads<2>(Vt, lane, vr);
+#endif
     mask(s);
     if (first) m = xor32_max(max16(s));
     bf16x8 pf[2];
@@ -372,7 +424,11 @@ __device__ __forceinline__ void attn_step_lf(const char* Kt, const char* Vt, int
         expo(t);
     }
     lacc = ln;
+#if VPF_ATTN_VEARLY & 1
+    pv_mfmas<2>(vr, pf, o0, o1);
+#else
     pv32<2>(Vt, lane, pf, o0, o1);
+#endif
 }
 
 // The last key step when at most 8 of its 32 keys are real (attn_step_tail8's register map: s[0..3] only), in the
