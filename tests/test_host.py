@@ -166,6 +166,18 @@ def test_c_abi_rejects_bad_shapes_before_any_launch():
     assert sk(fake, 768, fake, fake, None, None, None, fake, 768, 4, 768, 768, 0, 5, None, fake, 10 ** 7, None) == -1
     assert sk(fake, 768, fake, fake, None, None, None, fake, 768, 4, 768, 768, 0, 3, None, fake, 100, None) == -1
     assert sk(fake, 768, fake, fake, None, None, None, fake, 768, 4, 768, 768, 4, 3, None, fake, 10 ** 7, None) == -1
+    sc = L.vpf_stats_combine
+    # (round 5) no planes; a plane stride shorter than the rows; a misaligned output; D = 0
+    assert sc(fake, 0, 100, 100, 768, 1e-6, fake, None) == -1
+    assert sc(fake, 12, 99, 100, 768, 1e-6, fake, None) == -1
+    assert sc(fake, 12, 100, 100, 768, 1e-6, fake + 4, None) == -1
+    assert sc(fake, 12, 100, 100, 0, 1e-6, fake, None) == -1
+    cr = L.vpf_crop_patches_bf16
+    norm = (ctypes.c_float * 6)(*([0.5] * 6))
+    # S not a multiple of the patch; Kp below 3 patch^2; Kp not a multiple of 8
+    assert cr(fake, 224, 224, fake, fake, 8, 8, 64.0, 64.0, 224, 15, 768, norm, fake, None) == -1
+    assert cr(fake, 224, 224, fake, fake, 8, 8, 64.0, 64.0, 224, 16, 760, norm, fake, None) == -1
+    assert cr(fake, 336, 336, fake, fake, 8, 8, 64.0, 64.0, 336, 14, 590, norm, fake, None) == -1
 
 
 def test_checkpoint_paths_round_trip():
