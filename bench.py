@@ -98,6 +98,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1: nccl (= RCCL over xGMI, the product path) or gloo "
                          "(host-staged; lets several ranks share one GPU to rehearse the multi-rank path)")
+    ap.add_argument("--dist-timeout", type=float, default=120.0,
+                    help="seconds: bound on the process-group rendezvous and on any collective (RCCL watchdog), so "
+                         "a broken multi-GPU start fails fast and names its rank (vpf.distributed)")
     ap.add_argument("--kernel-frames", type=int, default=2, help="eager frames timed per kernel (roofline)")
     ap.add_argument("--cpu-frame-budget", type=float, default=480.0,
                     help="seconds: a full CPU frame projected above this falls back to the bounded sample")
@@ -299,10 +302,10 @@ def main() -> int:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        # bounded rendezvous + one probe collective, rank / world / backend on stderr first
+        from vitparticlefiltertracker_amd.distributed import init_distributed
+        init_distributed(args.dist_backend, dev if args.dist_backend == "nccl" else None, args.dist_timeout, rank,
+                         world)
     if args.particles < world:
         raise SystemExit("--particles must be at least the number of ranks")
     if args.gpus != world and rank == 0:

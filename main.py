@@ -31,6 +31,8 @@ def main(argv=None) -> int:
     ap.add_argument("--checkpoint-every", type=int, default=0, help="also save every N frames")
     ap.add_argument("--resume", default=None,
                     help="continue from a checkpoint: the source's frames up to its frame index are skipped")
+    ap.add_argument("--dist-timeout", type=float, default=120.0,
+                    help="seconds: bound on the multi-GPU rendezvous and on any collective (vpf.distributed)")
     args = ap.parse_args(argv)
 
     import torch
@@ -40,10 +42,11 @@ def main(argv=None) -> int:
 
     cfg = load_config(args.config)
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
+        from vitparticlefiltertracker_amd.distributed import init_distributed
         dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         torch.cuda.set_device(dev)
-        # device_id binds the RCCL communicator to this rank's GPU eagerly (as bench.py does)
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL bound to this rank's GPU eagerly (device_id), a bounded rendezvous and one probe collective (as bench.py)
+        init_distributed("nccl", dev, args.dist_timeout)
     inp = cfg["input"]
     n = args.frames or int(inp["frames"])
     if inp["source"] == "synthetic":

@@ -2,7 +2,11 @@
 scaling run that proves the ranks saw one global weight set and agree on the estimate and the resample. Each rank
 holds a stand-in filter (the attributes the check reads: the estimate, the global CDF it computed, its ancestor
 slots) built from one shared global weight vector; the check must pass when they are consistent and fail when a
-rank's estimate, CDF or ancestor range disagrees."""
+rank's estimate, CDF or ancestor range disagrees.
+
+Also the fail-fast start of the N > 1 path (`vitparticlefiltertracker_amd/distributed.py`, used by
+bench.py and main.py): on gloo, the bounded timeout is passed, the probe collective runs, rank / world / backend are
+printed before anything blocks, and a rank whose partner never arrives fails within the timeout, naming itself."""
 import os
 import socket
 import sys
@@ -58,9 +62,10 @@ class _FakeTracker:
 def _worker(rank, world, port, P, fault, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    from vitparticlefiltertracker_amd.distributed import init_distributed
+    init_distributed("gloo", None, 30.0, rank, world)     # what bench.py does at N > 1 (bounded, probed)
     try:
-        sys.path.insert(0, ROOT)
         import bench
         res = bench.multi_rank_check(_FakeTracker(_FakePF(rank, world, P, fault)), world, rank, "cpu", "gloo")
         q.put((rank, res))
@@ -112,3 +117,52 @@ def test_cpu_full_frame_measures_or_falls_back_within_budget():
     assert abs(full["value"] * full["s_per_frame"] - 1.0) < 0.02
     fb = bench.cpu_full_frame("vit_tiny_patch16_224", 48, 2, 1.0, budget_s=1e-6)
     assert fb["measured"].startswith("bounded sample") and fb["s_per_frame"] > 0 and fb["kind"] == "port"
+
+
+def _init_worker(rank, world, port, timeout_s, q):
+    import contextlib
+    import io
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    from vitparticlefiltertracker_amd.distributed import init_distributed
+    err = io.StringIO()
+    t0 = time.perf_counter()
+    try:
+        with contextlib.redirect_stderr(err):
+            r, w, probe_ms = init_distributed("gloo", None, timeout_s, rank, world)
+        q.put((rank, {"ok": True, "world": w, "probe_ms": probe_ms, "stderr": err.getvalue()}))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, {"ok": False, "error": repr(e), "seconds": time.perf_counter() - t0, "stderr": err.getvalue()}))
+
+
+def _run_init(world, started, timeout_s):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_init_worker, args=(r, world, port, timeout_s, q)) for r in range(started)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    return out
+
+
+def test_init_distributed_gloo_prints_and_probes():
+    out = _run_init(2, 2, 30.0)
+    for r, res in out.items():
+        assert res["ok"] and res["world"] == 2, (r, res)
+        assert f"rank {r} / world 2, backend gloo" in res["stderr"] and "timeout 30 s" in res["stderr"]
+        assert "probe all_reduce" in res["stderr"] and res["probe_ms"] >= 0.0
+
+
+def test_init_distributed_missing_rank_fails_within_timeout():
+    """World 2 with only rank 0 started: the rendezvous gives up after the bounded timeout (3 s here, 120 s in
+    bench.py) instead of torch's default, and the failure line names the rank, world and backend."""
+    out = _run_init(2, 1, 3.0)
+    res = out[0]
+    assert not res["ok"] and res["seconds"] < 30.0, res
+    assert "FAILED" in res["stderr"] and "rank 0 / world 2, backend gloo" in res["stderr"], res

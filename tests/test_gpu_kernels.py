@@ -589,10 +589,11 @@ def _attn_ref64(qkv, H):
 def test_attention_bf16_large(B, N, H):
     """B*H >= 4 x CUs; (4096, 197, 12) is the configs[1] launch. N <= 256 runs the key-pipelined kernel (with the
     16-query tail strip when the last strip holds <= 16 real queries: N = 197 / 111 / 33). N > 256 runs the key-streamed
-    kernel (round 5): 6-strip query blocks, K / V through a 9-chunk ring. N = 577 (configs[3], 64 x 16 units): 3 blocks
-    and the 16-query strip of query 576 on wave 0 of the last block beside its 32-query strip; N = 400: the same with
-    16 tail queries; N = 300: the 16-query strip on a wave of its own; N = 280: a partial 32-query strip; N = 640: a
-    4th block of 2 strips. Against an fp64 reference on at most 512 particles:
+    kernel (round 5): 4-wave workgroups of 4 x 32-query strips, K / V through a ring of 6 chunk slots (3 groups of 2
+    chunks). N = 577 (configs[3], 64 x 16 units): 5 blocks, the last with 2 strips and the 16-query strip of query 576
+    on a wave of its own; N = 400: 3 blocks, the 16-query strip (16 tail queries) on wave 0 of the last block beside its
+    32-query strip; N = 300: 3 blocks, the 16-query strip on a wave of its own; N = 280: a partial 32-query strip;
+    N = 640: 5 full blocks. Against an fp64 reference on at most 512 particles:
     every element within bf16 output rounding plus the bf16 probabilities' error, and no non-finite value anywhere
     (the round-2 stale-register NaN). q_rows = 1 (the CLS kernel) likewise."""
     torch.manual_seed(N + H)

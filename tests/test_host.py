@@ -251,17 +251,23 @@ def test_fp8_frame_flop_split():
 
 
 def test_checkpoint_formats_are_refused_with_a_reason():
-    """the weights' crc32 joined the fingerprint in round 4, so the format is now 3; format 1 and format 2
-    files get an explicit 're-create the checkpoint' message instead of a generic configuration mismatch."""
+    """the weights' crc32 joined the fingerprint in round 4, so the format is now 3; format 1 files and
+    format-2 files without the crc get an explicit 're-create the checkpoint' message instead of a generic
+    configuration mismatch. ADVICE r5: a format-2 file that carries the crc (round 4 wrote it without a format bump) is
+    checked like format 3, its crc included."""
     import json
     from vitparticlefiltertracker_amd.tracker import CHECKPOINT_FORMAT, _check_fingerprint
     assert CHECKPOINT_FORMAT == 3
     mine = {"arch": "vit_tiny_patch16_224", "weights_crc32": "0123abcd", "P": 16}
     cfg = np.array(json.dumps(mine))
+    no_crc = np.array(json.dumps({k: v for k, v in mine.items() if k != "weights_crc32"}))
     _check_fingerprint({"format": np.int64(3), "config": cfg}, mine)
-    for fmt, words in ((1, "format 1"), (2, "crc32")):
+    _check_fingerprint({"format": np.int64(2), "config": cfg}, mine)
+    with pytest.raises(ValueError, match="weights_crc32"):
+        _check_fingerprint({"format": np.int64(2), "config": cfg}, {**mine, "weights_crc32": "ffffffff"})
+    for fmt, c, words in ((1, cfg, "format 1"), (2, no_crc, "predates the weights' crc32")):
         with pytest.raises(ValueError, match=words):
-            _check_fingerprint({"format": np.int64(fmt), "config": cfg}, mine)
+            _check_fingerprint({"format": np.int64(fmt), "config": c}, mine)
     with pytest.raises(ValueError, match="weights_crc32"):
         _check_fingerprint({"format": np.int64(3), "config": cfg}, {**mine, "weights_crc32": "ffffffff"})
     with pytest.raises(ValueError, match="unknown"):
@@ -299,6 +305,8 @@ def test_attention_q_loads_are_waited_before_any_use(tmp_path):
     checked = 0
     for f in funcs:
         name = f.split(":", 1)[0]
+        if not name.startswith("_Z"):     # the module header before the first kernel (it names them in .globl lines)
+            continue
         if "k_attn_bf16_pipe" not in name and "k_attn_stream" not in name:
             continue
         L = [ln.strip() for ln in f.splitlines()]
@@ -314,6 +322,39 @@ def test_attention_q_loads_are_waited_before_any_use(tmp_path):
         assert not touched, (name, touched[:4])
         checked += 1
     assert checked == 3, checked
+
+
+def test_attention_bf16_and_mx8_instances_share_the_step_form(tmp_path):
+    """the MX8-output attention (fp8 path) must equal quantize_mx8 of the bf16-output attention bit for
+    bit (tests/test_gpu_mx8.py), which holds only while both k_attn_bf16_pipe instances run the same 32-query step
+    arithmetic. Round 5's red GPU run (gpurun_out/r5b, 3 x 197 x 12) came from a tree in which the N <= 256 kernel's
+    32-query strips ran attn_step_lf (l summed from the bf16 probabilities on 4x4x4 MFMAs): the bf16 instance computes
+    queries 192..196 on the 16-query strip (fp32 l), the MX8 instance, which has no 16-query strip, on the 32-query
+    strip (then bf16-probability l), and the 3-bit e4m3 rounding exposed the difference. Checked on the compiled gfx950
+    code: neither instance contains a 4x4x4 MFMA (the lf step form), and both carry the same number of 32x32x16 MFMAs
+    (the same 32-query steps); only the bf16 instance has the 16-query strip's 16x16x32 MFMAs."""
+    import collections
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(ROOT, "vitparticlefiltertracker_amd", "csrc", "attention.hip")
+    out = tmp_path / "attention.s"
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-function", "--cuda-device-only",
+                    "-S", "-o", str(out), src], check=True, capture_output=True)
+    counts = {}
+    for f in re.split(r"\n(?=_Z\S*:)", out.read_text()):
+        name = f.split(":", 1)[0]
+        if name.startswith("_Z") and "k_attn_bf16_pipe" in name:
+            out8 = "Lb1E" in name
+            counts[out8] = collections.Counter(ln.split()[0] for ln in map(str.strip, f.splitlines())
+                                               if ln.startswith("v_mfma"))
+    assert set(counts) == {False, True}, counts
+    for c in counts.values():
+        assert not any(k.startswith("v_mfma_f32_4x4x4") for k in c), counts
+    assert counts[False]["v_mfma_f32_32x32x16_bf16"] == counts[True]["v_mfma_f32_32x32x16_bf16"] > 0, counts
+    assert counts[False]["v_mfma_f32_16x16x32_bf16"] > 0 and counts[True]["v_mfma_f32_16x16x32_bf16"] == 0, counts
 
 
 def test_config_bboxes_validation():

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Build A/B variants of libvpf.so into ab_libs/ (travels to the GPU box; git-ignored): the crop's LDS window size in
-# dwords (cropN); the attention steps' early V reads (vearlyN: bit 1 the N > 256 steps, bit 2 the N <= 256 ones). The attention chunks-per-barrier (VPF_ATTN_CPB) and GEMM refill-spacing (VPF_ILV_SPACING) macros of
-# rounds 1-3 are in the lab snapshots (tools/gemm_lab/*_lab.hip); the product sources fix them (6 and 16).
+# dwords (cropN). The attention's early-V-read switch (round 5's vearlyN) left the product source in round 6 (the N > 256
+# steps always read early, the N <= 256 ones never: profiles/r5_lab/attn_vearly_ab.txt). The attention chunks-per-barrier
+# (VPF_ATTN_CPB) and GEMM refill-spacing (VPF_ILV_SPACING) macros of rounds 1-3 are in the lab snapshots
+# (tools/gemm_lab/*_lab.hip); the product sources fix them (6 and 16).
 # usage: bash tools/ab_libs.sh cpb2 crop10240 ...   then  VPF_LIB_PATH=ab_libs/libvpf_cpb2.so python bench.py ...
 set -e
 cd "$(dirname "$0")/.."
@@ -11,7 +13,6 @@ F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -fvisibility=hidden"
 for v in "$@"; do
   case $v in
     crop*) src=crop; def="-DVPF_CROP_LDS_DW=${v#crop}" ;;
-    vearly*) src=attention; def="-DVPF_ATTN_VEARLY=${v#vearly}" ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
   OBJS=""

@@ -15,7 +15,8 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    from vitparticlefiltertracker_amd.distributed import init_distributed
+    init_distributed("nccl", torch.device("cuda", dev), 120.0, rank, world)
     x = torch.full((4,), rank + 1, device="cuda", dtype=torch.int32)
     out = torch.empty(4 * world, device="cuda", dtype=torch.int32)
     dist.all_gather_into_tensor(out, x)

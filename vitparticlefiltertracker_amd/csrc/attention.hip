@@ -250,13 +250,11 @@ __device__ __forceinline__ void pv32(const char* Vt, int lane, const bf16x8 pf[2
         }
 }
 
-// pv32 split in two (VPF_ATTN_VEARLY: bit 1 the attn_step_lf steps, bit 2 attn_step_pl): the V^T fragment reads, issued right after a step's QK^T MFMAs so their latency
-// hides under the softmax, and the MFMAs behind the wait that retires them. The reads are inline asm like pv32's: the
-// builtin form made hipcc drain vmcnt(0) (every K / V DMA group in flight) before the first of them. The same reads
-// and MFMAs in the same order as pv32: bit-identical.
-#ifndef VPF_ATTN_VEARLY
-#define VPF_ATTN_VEARLY 1   // product: the N > 256 kernel's steps (-1 % at N = 577, r5_lab/attn_vearly_ab.txt)
-#endif
+// pv32 split in two for the N > 256 kernel's steps (attn_step_lf): the V^T fragment reads, issued right after a step's
+// QK^T MFMAs so their latency hides under the softmax, and the MFMAs behind the wait that retires them (-1 % at N = 577,
+// bit-identical, profiles/r5_lab/attn_vearly_ab.txt; at N = 197 the same move was level and spilled at 128 VGPRs, so
+// attn_step_pl keeps pv32). The reads are inline asm like pv32's: the builtin form made hipcc drain vmcnt(0) (every
+// K / V DMA group in flight) before the first of them. The same reads and MFMAs in the same order as pv32.
 template <int HALVES>
 __device__ __forceinline__ void pv_reads(const char* Vt, int lane, bf16x4 (&vr)[2][2][2]) {
     const int grp = lane >> 4, gi = lane & 15;
@@ -297,10 +295,6 @@ __device__ __forceinline__ void attn_step_pl(const char* Kt, const char* Vt, int
                                              float scale_log2, float& m, float& l, f32x16& o0, f32x16& o1) {
     const int hh = lane >> 5;
     f32x16 s = qk32(Kt, lane, qf);
-#if VPF_ATTN_VEARLY & 2
-    bf16x4 vr[2][2][2];
-    pv_reads<2>(Vt, lane, vr);
-#endif
     float bm = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -330,11 +324,7 @@ __device__ __forceinline__ void attn_step_pl(const char* Kt, const char* Vt, int
     for (int st = 0; st < 2; ++st)
         pf[st] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf2(s[8 * st + 0], s[8 * st + 1]), pack_bf2(s[8 * st + 2], s[8 * st + 3]),
                                                        pack_bf2(s[8 * st + 4], s[8 * st + 5]), pack_bf2(s[8 * st + 6], s[8 * st + 7])));
-#if VPF_ATTN_VEARLY & 2
-    pv_mfmas<2>(vr, pf, o0, o1);
-#else
     pv32<2>(Vt, lane, pf, o0, o1);
-#endif
 }
 
 // attn_step_tail8 of rounds 1-4 (at most 8 real keys in the tile: s[0..3] only, the first 16-key PV half)
@@ -391,10 +381,8 @@ __device__ __forceinline__ void attn_step_lf(const char* Kt, const char* Vt, int
         }
     };
     f32x16 s = qk32(Kt, lane, qf);
-#if VPF_ATTN_VEARLY & 1
     bf16x4 vr[2][2][2];
     pv_reads<2>(Vt, lane, vr);
-#endif
     mask(s);
     if (first) m = xor32_max(max16(s));
     bf16x8 pf[2];
@@ -424,11 +412,7 @@ __device__ __forceinline__ void attn_step_lf(const char* Kt, const char* Vt, int
         expo(t);
     }
     lacc = ln;
-#if VPF_ATTN_VEARLY & 1
     pv_mfmas<2>(vr, pf, o0, o1);
-#else
-    pv32<2>(Vt, lane, pf, o0, o1);
-#endif
 }
 
 // The last key step when at most 8 of its 32 keys are real (attn_step_tail8's register map: s[0..3] only), in the
@@ -686,38 +670,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 // ---------------- N > 256 (ViT-L/14 @ 336: N = 577): K / V streamed through a ring, queries in blocks ----------------
 // The N <= 256 kernel keeps a head's whole K / V image in LDS (57 KiB at N = 197); at N = 577 that image is 152 KiB, so
 // one workgroup fits a CU, its load phase is not overlapped, and 19 strips over 8 waves leave the SIMDs unbalanced
-// (round 1-4: 9.93 ms per launch at 4096 x 16 heads = 0.225 of the bf16 peak). Here:
-//  * one workgroup = WAVES (6) waves = one 192-query block of one (particle, head): QB = 3 blocks cover the 576 queries
-//    of the 18 full 32-query strips. The 16-query strip (N = 577: query 576 alone) rides on wave 0 of the last block
-//    (attn_step16 beside its 32-query strip) or on a wave of that block that has no 32-query strip.
-//  * K / V arrive in 32-key chunks (4 KiB of K + 4 KiB of V) through a ring of 9 chunk slots (72 KiB: two workgroups
-//    per CU, 12 waves = 3 per SIMD, 168 VGPRs per wave). A group of 3 chunks = 24 LDS-DMA pieces of 1 KiB, 4 per wave;
-//    three groups are resident: while one is computed, the next two are in flight. One counted vmcnt + s_barrier per
-//    group; after the barrier of group g every wave has finished group g - 1, whose slots take group g + 2.
-//  * the three blocks of a unit run on one XCD (blockIdx b -> XCD b % 8; consecutive blocks of that XCD are one unit's
-//    blocks), so two of the three K / V reads of a unit are L2 hits.
-//  * the steps are attn_step_lf (l on the matrix cores, speculative max), addressed by slot.
-// Per unit the work is 18 strips x 19 key steps (+ the 16-query strip); a row's bits depend on N only, not on q_rows
-// or on the block it falls in.
-// WAVES x CPB: 4 x 2 (product: a 4-wave workgroup has one wave on each SIMD whatever the dispatcher does, 3 workgroups
-// of 48 KiB per CU) or 6 x 3 (72 KiB, 2 per CU); LF: the attn_step_lf steps (else attn_step_pl). Compile-time choices
-// (lab A/B builds define them), not run-time knobs.
-#ifndef VPF_STREAM_WAVES
-#define VPF_STREAM_WAVES 4
-#endif
-#ifndef VPF_STREAM_LF
-#define VPF_STREAM_LF 1
-#endif
-constexpr int STREAM_WAVES = VPF_STREAM_WAVES;
-constexpr int STREAM_CPB = STREAM_WAVES == 4 ? 2 : 3;   // 32-key chunks per group (8 pieces each: 4 per wave per group)
+// (rounds 1-4: 9.93 ms per launch at 4096 x 16 heads = 0.225 of the bf16 peak). Here (round 5):
+//  * one workgroup = 4 waves = one 128-query block of one (particle, head): QB = 5 blocks cover N = 577 (four blocks of
+//    4 x 32-query strips, then 2 strips, and the 16-query strip of query 576 on a wave of its own, attn_step16). A
+//    4-wave workgroup has one wave on each SIMD whatever the dispatcher does (6-wave workgroups land 2/4/3/3 per SIMD,
+//    tools/micro/simd_probe.hip).
+//  * K / V arrive in 32-key chunks (4 KiB of K + 4 KiB of V) through a ring of 6 chunk slots (48 KiB: three workgroups
+//    per CU, one wave of each on every SIMD). A group of 2 chunks = 16 LDS-DMA pieces of 1 KiB, 4 per wave; three groups
+//    are resident: while one is computed, the next two are in flight. One counted vmcnt + s_barrier per group; after the
+//    barrier of group g every wave has finished group g - 1, whose slots take group g + 2.
+//  * the blocks of a unit run on one XCD (blockIdx b -> XCD b % 8; consecutive blocks of that XCD are one unit's blocks),
+//    so four of the five K / V reads of a unit are L2 hits.
+//  * the steps are attn_step_lf (l on the matrix cores, speculative max, early V^T reads).
+// A row's bits depend on N only, not on q_rows or on the block it falls in. The variants measured against this form in
+// round 5 (6-wave / 3-chunk workgroups, the attn_step_pl steps, software pipelining, two strips per wave) are recorded
+// in profiles/r5_lab/attn_stream_*_ab.txt; the product compiles this form only.
+constexpr int STREAM_WAVES = 4;
+constexpr int STREAM_CPB = 2;                      // 32-key chunks per group (8 pieces each: 4 per wave per group)
 constexpr int STREAM_RING = 3;                     // groups resident in the ring
+constexpr int STREAM_SLOTS = STREAM_CPB * STREAM_RING;
 
-template <int WAVES, int CPB, bool LF>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void k_attn_stream(
+__global__ __launch_bounds__(STREAM_WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void k_attn_stream(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows, int QB,
     int BH) {
-    constexpr int STREAM_CPB = CPB;
-    constexpr int STREAM_SLOTS = CPB * STREAM_RING;
+    constexpr int WAVES = STREAM_WAVES;
     constexpr int STREAM_LDS = STREAM_SLOTS * 2 * 4096;
     static_assert((STREAM_CPB * 8) % WAVES == 0, "a group's DMA pieces split evenly over the waves");
     constexpr int PPW = STREAM_CPB * 8 / WAVES;    // DMA pieces per wave per group
@@ -754,7 +730,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(q16[kk]) : "v"(qp16 + kk * 32));
     }
-    // group g = chunks [3g, 3g + 3): piece pi = 0..23 of a group is chunk pi / 8, K (pi & 4 == 0) or V, rows 8 (pi & 3) ..
+    // group g = chunks [2g, 2g + 2): piece pi = 0..15 of a group is chunk pi / 8, K (pi & 4 == 0) or V, rows 8 (pi & 3) ..
     // + 7 of that chunk (one 1 KiB wave-instruction, lane-linear destination, swizzle on the source address as in
     // k_attn_bf16_pipe); wave w issues pieces w, w + WAVES, ... Rows >= N read row N - 1 (finite; masked keys).
     auto issue_group = [&](int g) {
@@ -785,7 +761,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
 
     f32x16 o0 = {}, o1 = {};
     f32x4 lacc = {};
-    float m = -INFINITY, l = 0.f;
+    float m = -INFINITY;
     f32x4 o16[4] = {};
     float m16 = -INFINITY, l16 = 0.f;
     const int nfull = N >> 5;                      // chunks without padded keys
@@ -802,10 +778,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
             const int sl = c % STREAM_SLOTS;
             const char* Kt = Ks + sl * 4096;
             const char* Vt = Vs + sl * 4096;
-            if (act32) {
-                if constexpr (LF) attn_step_lf<false>(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
-                else attn_step_pl<false>(Kt, Vt, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-            }
+            if (act32) attn_step_lf<false>(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
             if (act16) attn_step16<false>(Kt, Vt, c * 32, N, lane, q16, scale_log2, m16, l16, o16);
         }
     }
@@ -814,13 +787,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
         const char* Kt = Ks + sl * 4096;
         const char* Vt = Vs + sl * 4096;
         if (act32) {
-            if constexpr (LF) {
-                if (N - c * 32 <= 8) attn_step_tail8_lf(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
-                else attn_step_lf<true>(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
-            } else {
-                if (N - c * 32 <= 8) attn_step_tail8_pl(Kt, Vt, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-                else attn_step_pl<true>(Kt, Vt, c * 32, N, lane, qf, scale_log2, m, l, o0, o1);
-            }
+            if (N - c * 32 <= 8) attn_step_tail8_lf(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
+            else attn_step_lf<true>(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
         }
         if (act16) attn_step16<true>(Kt, Vt, c * 32, N, lane, q16, scale_log2, m16, l16, o16);
     }
@@ -836,7 +804,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
         }
     }
     if (!act32) return;
-    const float inv = 1.0f / xor32_sum(LF ? lacc[0] : l);
+    const float inv = 1.0f / xor32_sum(lacc[0]);
     uint32_t gx[8], gy[8];   // as k_attn_bf16_pipe: permlane32 pairs -> one 16-B store per 8-dim pair
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1034,10 +1002,7 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     // N <= 256: the key-pipelined kernel (8 waves, one strip each, the head's whole K / V image in LDS); N > 256: the
     // key-streamed, query-blocked kernel. (Round 4's persistent chunk-ring form of the N <= 256 kernel is bit-identical
     // but 1.5x slower: tools/gemm_lab/attention_lab.hip, profiles/r4_lab/attn_ring_ab_v*.txt.)
-#ifndef VPF_ATTN_STREAM_MIN_N   // LAB A/B only: route N >= this to the key-streamed kernel (product: N > 256)
-#define VPF_ATTN_STREAM_MIN_N 257
-#endif
-    if (N < VPF_ATTN_STREAM_MIN_N) {
+    if (N <= 256) {
         static bool pipe_attr = false;   // benign race: idempotent attribute set
         if (!pipe_attr) {
             (void)hipFuncSetAttribute((const void*)k_attn_bf16_pipe<PIPE_CPB, false>,
@@ -1055,7 +1020,7 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     const int QB = need > W ? (need + W - 1) / W : 1;
     const int64_t blocks = (BH + 7) / 8 * 8 * QB;
     if (blocks > INT32_MAX) return VPF_ERR_ARG;
-    hipLaunchKernelGGL((k_attn_stream<W, STREAM_CPB, VPF_STREAM_LF != 0>), dim3((unsigned)blocks), dim3(64 * W), 0,
+    hipLaunchKernelGGL(k_attn_stream, dim3((unsigned)blocks), dim3(64 * W), 0,
                        (hipStream_t)stream,
                        reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<bf16_t*>(out), N, H, scale_log2, q_rows,
                        QB, (int)BH);

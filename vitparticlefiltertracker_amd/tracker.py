@@ -88,18 +88,20 @@ def _stage_frame(self, frame) -> torch.Tensor:
 
 
 class _LazyDigest:
-    """`weights_digest` of the tracker's weights, computed on first use (a checkpoint save / load) and cached: the crc32
-    converts every weight to a host fp32 copy (~1.2 GB for ViT-L/14), which a tracker that never checkpoints should not
-    pay at construction. Weights built from the seed are rebuilt from it (make_vit_weights is
-    deterministic); weights passed in are the caller's tensors, referenced, not copied."""
+    """`weights_digest` of the tracker's weights. Weights built from the seed: computed on first use (a checkpoint save /
+    load) from a rebuild (make_vit_weights is deterministic) and cached, since the crc32 converts every weight to a host
+    fp32 copy (~1.2 GB for ViT-L/14) that a tracker which never checkpoints should not pay. Weights passed
+    in: digested at construction (`_set_weights_digest`) and not referenced afterwards, so the caller can free them and
+    a later change to the caller's tensors cannot make the recorded crc describe other weights than the engine's copy
+    (ADVICE r5)."""
+
+    def _set_weights_digest(self, weights) -> None:
+        self._digest = weights_digest(weights) if weights is not None else None
 
     @property
     def weights_digest(self) -> str:
         if self._digest is None:
-            w = self._weights_arg
-            if w is None:
-                w = make_vit_weights(self.arch, seed=int(self.cfg["model"]["weights"]["seed"]))
-            self._digest = weights_digest(w)
+            self._digest = weights_digest(make_vit_weights(self.arch, seed=int(self.cfg["model"]["weights"]["seed"])))
         return self._digest
 
 
@@ -123,17 +125,27 @@ def _check_fingerprint(sd: dict, mine: dict) -> None:
         raise ValueError("checkpoint format 1 (rounds 1-2) records only P, rank, world size, seed and arch; format "
                          f"{CHECKPOINT_FORMAT} also checks every value the tracking arithmetic depends on (dtype, lambda, "
                          "motion, weights, ...): re-create the checkpoint with this version")
-    if fmt == 2:
-        raise ValueError("checkpoint format 2 (round 4) does not record the weights' crc32, which format "
-                         f"{CHECKPOINT_FORMAT} checks so that a resume with other weights is refused: re-create the "
-                         "checkpoint with this version")
-    if fmt != CHECKPOINT_FORMAT:
+    if fmt not in (2, CHECKPOINT_FORMAT):
         raise ValueError(f"unknown checkpoint format {fmt}")
     saved = json.loads(str(sd["config"]))
+    # format 2 is format 3 without the bump (round 4 added the crc to format 2's fingerprint): such a file carries the
+    # crc and is checked like format 3; a format-2 file written before that lacks it and is refused
+    if fmt == 2 and "weights_crc32" not in saved:
+        raise ValueError("this format-2 checkpoint predates the weights' crc32 in the fingerprint, which format "
+                         f"{CHECKPOINT_FORMAT} checks so that a resume with other weights is refused: re-create the "
+                         "checkpoint with this version")
     diff = sorted(k for k in set(saved) | set(mine) if saved.get(k) != mine.get(k))
     if diff:
         raise ValueError("checkpoint was written by a tracker with another configuration or rank layout: "
                          + ", ".join(f"{k} {saved.get(k)!r} != {mine.get(k)!r}" for k in diff))
+
+
+def _sd_particles_soa(sd: dict) -> np.ndarray:
+    """A checkpoint's particle states in the SoA layout (float32[3][P_l], [K][3][P_l] for a MultiTracker). Since round 6
+    the key is `particles_soa`: `ParticleFilter.particles` became the [P_l][3] view in round 5, and one name for two
+    shapes invited misreads. Files of earlier rounds store the same SoA array under `particles`."""
+    a = sd["particles_soa"] if "particles_soa" in sd else sd["particles"]
+    return np.ascontiguousarray(a, dtype=np.float32)
 
 
 def _checkpoint_file(path: str, rank: int, world_size: int) -> str:
@@ -175,7 +187,7 @@ class Tracker(_LazyDigest):
         P = int(c["particles"]["num"])
         _, self.n_local = shard_range(P, self.world_size, self.rank)   # rank r: [floor(rP/G), floor((r+1)P/G))
         w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
-        self._weights_arg, self._digest = weights, None
+        self._set_weights_digest(weights)
         self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, max(1, self.n_local),
                                 c["model"]["mean"], c["model"]["std"])
         self.lam = float(c["likelihood"]["lambda"])
@@ -278,8 +290,9 @@ class Tracker(_LazyDigest):
         return _fingerprint(self.cfg, self.arch.name, self.weights_digest, self.rank, self.world_size)
 
     def state_dict(self) -> dict:
-        """The tracker's state between frames as numpy arrays: this rank's particles (after the last resample, so
-        Q is zero), the template, the template box, the frame size and the frame index, plus the configuration
+        """The tracker's state between frames as numpy arrays: this rank's particles as `particles_soa` (float32[3][P_l],
+        the SoA storage; `ParticleFilter.particles` is its [P_l][3] view) after the last resample (so Q is zero), the
+        template, the template box, the frame size and the frame index, plus the configuration
         fingerprint (JSON). The motion noise and the resample word are counter-based (seed, frame index, global
         particle index: SPEC S1/S2), so a tracker with the same configuration that loads this continues bit for
         bit."""
@@ -287,7 +300,7 @@ class Tracker(_LazyDigest):
         if self.pf is None:
             raise RuntimeError("call init(frame, bbox) first")
         return {"format": np.int64(CHECKPOINT_FORMAT), "frame_index": np.int64(self.frame_index),
-                "pf_frame": np.int64(self.pf.frame), "particles": self.pf.particles_soa.cpu().numpy(),
+                "pf_frame": np.int64(self.pf.frame), "particles_soa": self.pf.particles_soa.cpu().numpy(),
                 "template": self.template.cpu().numpy(), "box_wh": np.array(self.box_wh, np.float64),
                 "frame_hw": np.array([self.pf.height, self.pf.width], np.int64),
                 "config": np.array(json.dumps(self.config_fingerprint(), sort_keys=True))}
@@ -310,7 +323,7 @@ class Tracker(_LazyDigest):
                                      self.lam, self.bits, self.rank, self.world_size, self.group)
         self.pf.reset((0.0, 0.0, 1.0))
         self.pf.height, self.pf.width = H, W
-        self.pf.particles_soa.copy_(torch.from_numpy(np.ascontiguousarray(sd["particles"], dtype=np.float32)))
+        self.pf.particles_soa.copy_(torch.from_numpy(_sd_particles_soa(sd)))
         self.pf.frame = int(sd["pf_frame"])
         self.frame_index = int(sd["frame_index"])
         self._graph = None
@@ -370,7 +383,7 @@ class MultiTracker(_LazyDigest):
         self.P = int(c["particles"]["num"])
         _, self.n_local = shard_range(self.P, self.world_size, self.rank)
         w = weights if weights is not None else make_vit_weights(self.arch, seed=int(c["model"]["weights"]["seed"]))
-        self._weights_arg, self._digest = weights, None
+        self._set_weights_digest(weights)
         self.engine = ViTEngine(self.arch, w, c["model"]["dtype"], self.device, self.K * self.n_local,
                                 c["model"]["mean"], c["model"]["std"])
         self.lam = float(c["likelihood"]["lambda"])
@@ -466,14 +479,14 @@ class MultiTracker(_LazyDigest):
                 "n_objects": self.K}
 
     def state_dict(self) -> dict:
-        """Tracker.state_dict for every target: particles [K][3][P_l], templates [K][D], template boxes [K][2],
+        """Tracker.state_dict for every target: particles_soa [K][3][P_l], templates [K][D], template boxes [K][2],
         each filter's frame counter, the frame size and index, and the fingerprint (with the target count)."""
         import json
         if not self.pfs:
             raise RuntimeError("call init(frame, bboxes) first")
         return {"format": np.int64(CHECKPOINT_FORMAT), "n_objects": np.int64(self.K), "frame_index": np.int64(self.frame_index),
                 "pf_frame": np.array([pf.frame for pf in self.pfs], np.int64),
-                "particles": np.stack([pf.particles_soa.cpu().numpy() for pf in self.pfs]),
+                "particles_soa": np.stack([pf.particles_soa.cpu().numpy() for pf in self.pfs]),
                 "template": np.stack([t.cpu().numpy() for t in self.templates]),
                 "box_wh": np.array(self.boxes, np.float64),
                 "frame_hw": np.array([self.pfs[0].height, self.pfs[0].width], np.int64),
@@ -497,7 +510,7 @@ class MultiTracker(_LazyDigest):
         for k, pf in enumerate(self.pfs):
             pf.reset((0.0, 0.0, 1.0))
             pf.height, pf.width = H, W
-            pf.particles_soa.copy_(torch.from_numpy(np.ascontiguousarray(sd["particles"][k], dtype=np.float32)))
+            pf.particles_soa.copy_(torch.from_numpy(np.ascontiguousarray(_sd_particles_soa(sd)[k])))
             pf.frame = int(sd["pf_frame"][k])
             # in place: a captured graph reads these buffers
             self.templates[k].copy_(torch.from_numpy(np.ascontiguousarray(sd["template"][k], dtype=np.float32)))

@@ -385,8 +385,8 @@ class ViTEngine:
                 continue
             # the last block's attention reads only the CLS query: K, V for every row, Q for the CLS rows
             if fold:
-                s1, p1 = ln_stats(h2, st, pl)
                 if not last:
+                    s1, p1 = ln_stats(h2, st, pl)
                     _run(T, "gemm_qkv", vpf.gemm, h2, L["wqkv"], L["bqkv"], None, None, 0, s1, L["cqkv"], LNE, q2,
                          p1, eps)
                 elif self.cls_fused:
@@ -408,6 +408,9 @@ class ViTEngine:
                     _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # the CLS rows' {mean, rstd}
                     q_cls()
                 else:
+                    # the statistics only where a branch reads them: the CLS-fused and fp8 last blocks launch no
+                    # full-row combine (23 combines per frame where 22 are read)
+                    s1, p1 = ln_stats(h2, st, pl)
                     _run(T, "gemm_kv", vpf.gemm, h2, L["wqkv"][D:], L["bqkv"][D:], None, None, 0, s1, L["cqkv"][D:],
                          LNE, kv2, p1, eps)
                     _run(T, "row_stats", vpf.row_stats, hc, A.ln_eps, stc)     # the CLS rows' {mean, rstd}
