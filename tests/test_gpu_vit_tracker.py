@@ -182,6 +182,53 @@ def test_configs0_32_frame_clip_matches_oracle():
         np.testing.assert_allclose(e_gpu, e_ref, rtol=1e-12)
 
 
+def test_configs0_bf16_free_running_drift_vs_fp32_oracle():
+    """VERDICT r5 (parity caveat): the bf16 product tracker FREE-RUNNING — its own bf16 weights decide every resample —
+    against the fp32 CPU oracle free-running on the same configs[0] clip (256 particles, ViT-Ti/16, 32 frames; the same
+    seeds, so the two differ only through the bf16 forward's weights). Once one int64 weight differs the two filters
+    resample differently and their particle sets part, so this is a drift bound, not a parity bar: per frame the
+    estimates' |dx|, |dy| <= 4 px and |ds| <= 0.05 (round 6, first run: 1.99 / 1.45 px, 0.013). The distance of each
+    track from the target's true centre (frames.target_box) is reported, not asserted: with seeded random-init ViT
+    weights (no checkpoint offline) the features do not single out the target, and the fp32 oracle stays near the
+    start box exactly as the bf16 tracker does (both ~59 px behind the target by frame 31). The per-frame record goes
+    to $VPF_TEST_REPORT_DIR/bf16_drift_configs0.json when that is set (profiles/r6_bf16_drift_configs0.json)."""
+    import json
+    import os
+
+    from vitparticlefiltertracker_amd import Tracker
+    from vitparticlefiltertracker_amd.frames import target_box
+    cfg = _tiny_cfg(256, "bf16")
+    arch = ARCHS["vit_tiny_patch16_224"]
+    w = make_vit_weights(arch, seed=3)
+    clip = synthetic_clip(32)
+    bbox0 = (80, 80, 64, 64)
+    tr = Tracker(cfg, weights=w)
+    ot = OracleTracker(cfg, w, arch)                      # the fp32 CPU path (model.dtype is the GPU's only)
+    tr.init(clip[0], bbox0)
+    ot.init(clip[0], bbox0)
+    rows = []
+    for k, f in enumerate(clip[1:], start=1):
+        g = np.array(tr.track(f), np.float64)
+        r = np.array(ot.track(f), np.float64)
+        x, y, bw, bh = target_box(k, bbox0, (2, 1))
+        truth = np.array([x + 0.5 * bw, y + 0.5 * bh])
+        rows.append({"frame": k, "bf16": g.tolist(), "fp32_oracle": r.tolist(), "drift": (g - r).tolist(),
+                     "bf16_err_px": float(np.abs(g[:2] - truth).max()),
+                     "fp32_err_px": float(np.abs(r[:2] - truth).max())})
+    d = np.array([row["drift"] for row in rows])
+    summary = {"max_abs_dx": float(np.abs(d[:, 0]).max()), "max_abs_dy": float(np.abs(d[:, 1]).max()),
+               "max_abs_ds": float(np.abs(d[:, 2]).max()),
+               "max_bf16_err_px": max(row["bf16_err_px"] for row in rows),
+               "max_fp32_err_px": max(row["fp32_err_px"] for row in rows)}
+    rep = os.environ.get("VPF_TEST_REPORT_DIR")
+    if rep:
+        os.makedirs(rep, exist_ok=True)
+        with open(os.path.join(rep, "bf16_drift_configs0.json"), "w") as fh:
+            json.dump({"workload": "configs[0]: 256 particles, vit_tiny_patch16_224, 32-frame synthetic 224x224 clip",
+                       "summary": summary, "frames": rows}, fh, indent=1)
+    assert summary["max_abs_dx"] <= 4.0 and summary["max_abs_dy"] <= 4.0 and summary["max_abs_ds"] <= 0.05, summary
+
+
 @pytest.mark.parametrize("dtype,arch_name", [("bf16", "vit_tiny_patch16_224"), ("fp8", "vit_small_patch16_224")])
 def test_tracker_graph_equals_eager(dtype, arch_name):
     from vitparticlefiltertracker_amd import Tracker

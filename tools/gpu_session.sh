@@ -16,7 +16,7 @@ rocm-smi --showproductname > $OUT/gpu.txt 2>&1 || true
 for step in "$@"; do
   case $step in
     tests)
-      timeout -k 10 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 900 --timeout-method thread -rf ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1
+      VPF_TEST_REPORT_DIR=$OUT/reports timeout -k 10 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 900 --timeout-method thread -rf ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1
       ok_or_stop $? tests; tail -30 $OUT/pytest_gpu.log ;;
     host)   # the box's CPU share (bench.py cpu_baseline's core count) and model
       { echo "nproc=$(nproc) affinity=$(python3 -c 'import os;print(len(os.sched_getaffinity(0)))') OMP_NUM_THREADS=$OMP_NUM_THREADS";
@@ -118,6 +118,16 @@ for step in "$@"; do
     bench8)
       timeout -k 10 900 python bench.py --dtype fp8 --steps 5 --warmup 2 --cpu-baseline off > $OUT/bench8.log 2>&1
       ok_or_stop $? bench8; tail -1 $OUT/bench8.log | cut -c1-600 ;;
+    libab=*)   # libab=<variant>=<cases>: lib_ab.py against ab_libs/libvpf_<variant>.so (tools/variant_lib.py builds it)
+      IFS='=' read -r _ vname vcases <<< "$step"
+      timeout -k 10 600 python tools/lib_ab.py ${LIBAB_ROUNDS:-7} $vcases ab_libs/libvpf_$vname.so > $OUT/lib_ab_$vname.log 2>&1
+      ok_or_stop $? libab_$vname; grep -v amdgpu.ids $OUT/lib_ab_$vname.log ;;
+    nsweep)   # N <= 256 attention time per launch over token counts (tools/attn_nsweep.py)
+      timeout -k 10 300 python tools/attn_nsweep.py 7 ${NSWEEP_NS:-160,192,197,208,224,240,256} > $OUT/attn_nsweep.log 2>&1
+      ok_or_stop $? nsweep; grep -v amdgpu.ids $OUT/attn_nsweep.log ;;
+    benchq)   # the bench line without the CPU baseline (per-kernel table, roofline) for quick A/Bs of the product
+      timeout -k 10 600 python bench.py --steps 10 --warmup 3 --cpu-baseline off > $OUT/benchq.log 2>&1
+      ok_or_stop $? benchq; tail -1 $OUT/benchq.log | cut -c1-700 ;;
     libab)   # same-process A/B of the product library against LIBAB_LIB (default ab_libs/libvpf_direct.so)
       timeout -k 10 600 python tools/lib_ab.py ${LIBAB_ROUNDS:-7} ${LIBAB_CASES:-bf16_qkv,bf16_proj,bf16_fc1,bf16_fc2} ${LIBAB_LIB:-ab_libs/libvpf_direct.so} > $OUT/lib_ab.log 2>&1
       ok_or_stop $? libab; grep -v amdgpu.ids $OUT/lib_ab.log ;;

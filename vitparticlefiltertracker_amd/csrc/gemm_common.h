@@ -49,6 +49,16 @@ constexpr int TILE_BYTES = BM * 128;       // one operand K-tile: 256 rows x 128
 // A row-panels with the A panel index running fastest, so the ~32 tiles an XCD has in flight cover ~group A
 // panels x 32/group W panels and both stay in that XCD's L2 (profiles/r1_gemm_lab/group_sweep.txt).
 // group = 0: plain tm-major.
+// 16-B global store with the non-temporal hint (global_store_dwordx4 ... nt): for an output tile that no later tile of
+// this launch reads (the next kernel reads it from HBM anyway), so its lines need not displace the A / W panels the
+// XCD's other tiles re-read from L2. Used by store_wave_tile_pipe's non-residual epilogues (whole 128-B rows per
+// instruction): QKV -2.0 / -1.1 % in two same-process A/Bs; on the residual epilogues (proj, FC2) level, and on FC1's
+// direct stores (16 half rows per instruction) +4.3 %, so those keep the default policy
+// (profiles/r6_lab/gemm_ntstore_ab.txt, gemm_ntpipe_ab.txt).
+typedef unsigned u32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_nt(void* p, uint4 v) {
+    __builtin_nontemporal_store(u32x4_nt{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_nt*>(p));
+}
 // logical tile id -> output tile origin (the grouped order described above)
 __device__ __forceinline__ void tile_of_lid(int M, int N, int group, int lid, int& m0, int& n0) {
     const int tiles_n = (N + BN - 1) / BN;
@@ -247,7 +257,10 @@ __device__ __forceinline__ void store_wave_tile_pipe(char* img, const char* aux,
                     *reinterpret_cast<float2*>(img + row * 128 + c16 * 8) = make_float2(s1, s2);
                 }
             }
-            if (ok) *reinterpret_cast<uint4*>(Cl + (int64_t)(i * 16 + h) * ldc) = v;
+            if (ok) {
+                if constexpr (RES) *reinterpret_cast<uint4*>(Cl + (int64_t)(i * 16 + h) * ldc) = v;
+                else st16_nt(Cl + (int64_t)(i * 16 + h) * ldc, v);
+            }
         }
     }
     if constexpr (RES) {
