@@ -125,6 +125,13 @@ for step in "$@"; do
     nsweep)   # N <= 256 attention time per launch over token counts (tools/attn_nsweep.py)
       timeout -k 10 300 python tools/attn_nsweep.py 7 ${NSWEEP_NS:-160,192,197,208,224,240,256} > $OUT/attn_nsweep.log 2>&1
       ok_or_stop $? nsweep; grep -v amdgpu.ids $OUT/attn_nsweep.log ;;
+    dist2)   # the N > 1 start on one GPU: 2 ranks over gloo (the full bench path, rehearsal) and 2 ranks over RCCL, which
+             # RCCL refuses on one device: the run must end within its timeout, naming rank / world / backend
+      timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 --cpu-baseline off > $OUT/dist2_gloo.log 2>&1
+      ok_or_stop $? dist2_gloo; grep -h "vpf.distributed\|multi_rank_check" $OUT/dist2_gloo.log | cut -c1-300
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29518 tools/rccl_probe.py > $OUT/dist2_nccl_one_gpu.log 2>&1
+      echo "[dist2_nccl_one_gpu] rc=$? (expected non-zero: RCCL refuses two ranks on one device)" | tee -a $OUT/status.txt
+      grep -h "vpf.distributed\|Duplicate\|Error\|error" $OUT/dist2_nccl_one_gpu.log | head -12 | cut -c1-300 ;;
     benchq)   # the bench line without the CPU baseline (per-kernel table, roofline) for quick A/Bs of the product
       timeout -k 10 600 python bench.py --steps 10 --warmup 3 --cpu-baseline off > $OUT/benchq.log 2>&1
       ok_or_stop $? benchq; tail -1 $OUT/benchq.log | cut -c1-700 ;;
