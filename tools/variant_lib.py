@@ -32,8 +32,9 @@ def build(name: str) -> str:
     for fname, old, new in spec["EDITS"]:
         p = os.path.join(src, fname)
         text = open(p).read()
-        if old not in text:
-            raise SystemExit(f"variant {name}: edit target not found in {fname}: {old[:80]!r}")
+        if text.count(old) != 1:
+            raise SystemExit(f"variant {name}: edit target found {text.count(old)} times (need exactly 1) in {fname}: "
+                             f"{old[:80]!r}")
         open(p, "w").write(text.replace(old, new))
     defines = list(spec.get("DEFINES", []))
     objs = [os.path.join(work, f"{s}.o") for s in SRCS]
