@@ -250,6 +250,21 @@ def test_fp8_frame_flop_split():
     assert abs(big.gflop_per_crop_mx8() - 2 * 23 * (3 * Nl * Dl * Dl + 2 * Nl * Dl * Fl) / 1e9) < 1e-9
 
 
+def test_product_sources_have_no_compile_time_knobs():
+    """the product sources compile one form of each kernel. No preprocessor switch named VPF_* (the
+    round-1..5 lab knobs: VPF_STREAM_WAVES, VPF_STREAM_LF, VPF_ATTN_VEARLY, VPF_ATTN_STREAM_MIN_N, VPF_CROP_LDS_DW) may
+    select code in csrc/; A/B variants are text edits applied to a copy by tools/variant_lib.py."""
+    csrc = os.path.join(ROOT, "vitparticlefiltertracker_amd", "csrc")
+    bad = []
+    for name in sorted(os.listdir(csrc)):
+        if not name.endswith((".hip", ".h")):
+            continue
+        for i, line in enumerate(open(os.path.join(csrc, name)), 1):
+            if re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b.*\bVPF_", line):
+                bad.append(f"{name}:{i}: {line.strip()}")
+    assert not bad, bad
+
+
 def test_checkpoint_formats_are_refused_with_a_reason():
     """the weights' crc32 joined the fingerprint in round 4, so the format is now 3; format 1 files and
     format-2 files without the crc get an explicit 're-create the checkpoint' message instead of a generic

@@ -49,10 +49,7 @@ __device__ __forceinline__ float chan(uint32_t px, int c) { return (float)((px >
 // memory path, which bound the global form (the im2col stores are the same). A window larger than CROP_LDS_DW dwords
 // (a large template at a large scale) takes the global taps. Same per-value arithmetic (and order) as the generic
 // kernel and the oracle.
-#ifndef VPF_CROP_LDS_DW
-#define VPF_CROP_LDS_DW 10240   // -DVPF_CROP_LDS_DW=n builds A/B variants (tools/ab_libs.sh)
-#endif
-constexpr int CROP_LDS_DW = VPF_CROP_LDS_DW;   // 40 KiB: four workgroups per CU (0.45-0.49 vs 0.53 ms at 80 KiB and two per CU,
+constexpr int CROP_LDS_DW = 10240;   // 40 KiB: four workgroups per CU (0.45-0.49 vs 0.53 ms at 80 KiB and two per CU,
 // profiles/r2_gemm_lab/crop_lds_window_ab.txt); windows up to ~101 x 101 (a 64 x 64 template to scale ~1.55)
 // The particle's crop geometry and its source window (every bilinear tap of its S x S samples, clamped into the zero
 // border as rgba_tap does), staged into LDS when it fits; shared by both LDS kernels.
