@@ -303,8 +303,8 @@ def test_attention_q_loads_are_waited_before_any_use(tmp_path):
     DMAs with them), so nothing but the kernel's own shape orders them before their uses. Rounds 2 and 4 each broke
     that shape once (a phi of asm outputs: register copies of not-yet-landed loads, NaNs on the GPU). Here the device
     code of csrc/attention.hip is compiled to gfx950 assembly and, for both k_attn_bf16_pipe instances and the
-    key-streamed N > 256 kernel k_attn_stream (round 5: the 32-query strip's four loads and the 16-query strip's two):
-    * the Q loads are exactly four (six) asm global_load_dwordx4 into VGPRs;
+    key-streamed N > 256 kernel k_attn_stream (since round 6 also one load set for both strip kinds):
+    * the Q loads are exactly four asm global_load_dwordx4 into VGPRs;
     * between the last of them and the empty pin asm that follows the counted wait, there is at least one
       `s_waitcnt vmcnt` and no instruction names any VGPR those loads write (no copy, no read, no reuse)."""
     import shutil
@@ -327,7 +327,7 @@ def test_attention_q_loads_are_waited_before_any_use(tmp_path):
         L = [ln.strip() for ln in f.splitlines()]
         loads = [(i, _vregs(ln.split()[1].rstrip(","))) for i, ln in enumerate(L)
                  if ln.startswith("global_load_dwordx4 v[") and L[i - 1] == ";;#ASMSTART"]
-        assert len(loads) == (6 if "k_attn_stream" in name else 4), (name, loads)
+        assert len(loads) == 4, (name, loads)
         last = loads[-1][0]
         pin = next(i for i in range(last + 1, len(L) - 1) if L[i] == ";;#ASMSTART" and L[i + 1] == ";;#ASMEND")
         assert any(L[i].startswith("s_waitcnt") and "vmcnt" in L[i] for i in range(last, pin)), name

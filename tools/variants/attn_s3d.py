@@ -1,0 +1,5 @@
+"""k_attn_stream, strip kinds in separate loops: 2 chunk(s) per group, 3 groups resident, 3 waves per SIMD,
+attn_step_pl: False (tools/variants/_attn_split.py)."""
+import os
+import runpy
+EDITS = runpy.run_path(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_attn_split.py"))["edits"](2, 3, 3, False)

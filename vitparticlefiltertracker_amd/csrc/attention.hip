@@ -250,44 +250,6 @@ __device__ __forceinline__ void pv32(const char* Vt, int lane, const bf16x8 pf[2
         }
 }
 
-// pv32 split in two for the N > 256 kernel's steps (attn_step_lf): the V^T fragment reads, issued right after a step's
-// QK^T MFMAs so their latency hides under the softmax, and the MFMAs behind the wait that retires them (-1 % at N = 577,
-// bit-identical, profiles/r5_lab/attn_vearly_ab.txt; at N = 197 the same move was level and spilled at 128 VGPRs, so
-// attn_step_pl keeps pv32). The reads are inline asm like pv32's: the builtin form made hipcc drain vmcnt(0) (every
-// K / V DMA group in flight) before the first of them. The same reads and MFMAs in the same order as pv32.
-template <int HALVES>
-__device__ __forceinline__ void pv_reads(const char* Vt, int lane, bf16x4 (&vr)[2][2][2]) {
-    const int grp = lane >> 4, gi = lane & 15;
-    const int rq = gi >> 2, cp = gi & 3;
-    const int rbase = 4 * (grp >> 1) + rq;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-        const int col = dt * 32 + 16 * (grp & 1) + 4 * cp;
-        const uint32_t a = (uint32_t)(size_t)Vt + (uint32_t)(v_off(rbase, col >> 3) + (col & 7) * 2);
-        vr[0][dt][0] = ds_read_tr_asm_o<0>(a);
-        vr[0][dt][1] = ds_read_tr_asm_o<1024>(a);
-        if constexpr (HALVES == 2) {
-            vr[1][dt][0] = ds_read_tr_asm_o<2048>(a);
-            vr[1][dt][1] = ds_read_tr_asm_o<3072>(a);
-        }
-    }
-}
-template <int HALVES>
-__device__ __forceinline__ void pv_mfmas(bf16x4 (&vr)[2][2][2], const bf16x8 pf[2], f32x16& o0, f32x16& o1) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1]),
-                 "+v"(vr[1][0][0]), "+v"(vr[1][0][1]), "+v"(vr[1][1][0]), "+v"(vr[1][1][1])::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int st = 0; st < HALVES; ++st)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const bf16x4 lo = vr[st][dt][0], hi = vr[st][dt][1];
-            const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o0, 0, 0, 0);
-            else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], o1, 0, 0, 0);
-        }
-}
-
 // The same step in the rounds 1-4 form (the N <= 256 kernel's): the row max of every tile (T13 lazy rescale when it
 // moved by more than 2^8), l summed from the fp32 probabilities. Bit-identical to the rounds 1-4 attn_step.
 template <bool MASK>
@@ -381,8 +343,6 @@ __device__ __forceinline__ void attn_step_lf(const char* Kt, const char* Vt, int
         }
     };
     f32x16 s = qk32(Kt, lane, qf);
-    bf16x4 vr[2][2][2];
-    pv_reads<2>(Vt, lane, vr);
     mask(s);
     if (first) m = xor32_max(max16(s));
     bf16x8 pf[2];
@@ -412,7 +372,7 @@ __device__ __forceinline__ void attn_step_lf(const char* Kt, const char* Vt, int
         expo(t);
     }
     lacc = ln;
-    pv_mfmas<2>(vr, pf, o0, o1);
+    pv32<2>(Vt, lane, pf, o0, o1);
 }
 
 // The last key step when at most 8 of its 32 keys are real (attn_step_tail8's register map: s[0..3] only), in the
@@ -670,27 +630,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 // ---------------- N > 256 (ViT-L/14 @ 336: N = 577): K / V streamed through a ring, queries in blocks ----------------
 // The N <= 256 kernel keeps a head's whole K / V image in LDS (57 KiB at N = 197); at N = 577 that image is 152 KiB, so
 // one workgroup fits a CU, its load phase is not overlapped, and 19 strips over 8 waves leave the SIMDs unbalanced
-// (rounds 1-4: 9.93 ms per launch at 4096 x 16 heads = 0.225 of the bf16 peak). Here (round 5):
+// (rounds 1-4: 9.93 ms per launch at 4096 x 16 heads = 0.225 of the bf16 peak). Here (rounds 5-6):
 //  * one workgroup = 4 waves = one 128-query block of one (particle, head): QB = 5 blocks cover N = 577 (four blocks of
 //    4 x 32-query strips, then 2 strips, and the 16-query strip of query 576 on a wave of its own, attn_step16). A
 //    4-wave workgroup has one wave on each SIMD whatever the dispatcher does (6-wave workgroups land 2/4/3/3 per SIMD,
-//    tools/micro/simd_probe.hip).
-//  * K / V arrive in 32-key chunks (4 KiB of K + 4 KiB of V) through a ring of 6 chunk slots (48 KiB: three workgroups
-//    per CU, one wave of each on every SIMD). A group of 2 chunks = 16 LDS-DMA pieces of 1 KiB, 4 per wave; three groups
-//    are resident: while one is computed, the next two are in flight. One counted vmcnt + s_barrier per group; after the
-//    barrier of group g every wave has finished group g - 1, whose slots take group g + 2.
+//    tools/micro/simd_probe.hip). The 16-query strip always has a wave of its own: the host adds a block when every
+//    wave of the last one holds a 32-query strip (N % 32 in 1..16 with a multiple of 4 full strips, e.g. N = 400).
+//  * four workgroups per CU (round 6; round 5 ran three): one wave of each on every SIMD, so <= 128 VGPRs. A wave runs
+//    one strip kind (run_strip, instantiated per kind), so the 32-query strip's registers (o0 / o1 / lacc) and the
+//    16-query strip's (o16) are never live together, and one Q load set serves both kinds; the steps are attn_step_lf
+//    with the V^T reads after the softmax (126 VGPRs).
+//  * K / V arrive in 32-key chunks (4 KiB of K + 4 KiB of V) through a ring of 4 chunk slots (32 KiB per workgroup). A
+//    group of 2 chunks = 16 LDS-DMA pieces of 1 KiB, 4 per wave; two groups are resident: while one is computed, the
+//    next is in flight. One counted vmcnt + s_barrier per group; after the barrier of group g every wave has finished
+//    group g - 1, whose slots take group g + 1.
 //  * the blocks of a unit run on one XCD (blockIdx b -> XCD b % 8; consecutive blocks of that XCD are one unit's blocks),
 //    so four of the five K / V reads of a unit are L2 hits.
-//  * the steps are attn_step_lf (l on the matrix cores, speculative max, early V^T reads).
-// A row's bits depend on N only, not on q_rows or on the block it falls in. The variants measured against this form in
-// round 5 (6-wave / 3-chunk workgroups, the attn_step_pl steps, software pipelining, two strips per wave) are recorded
-// in profiles/r5_lab/attn_stream_*_ab.txt; the product compiles this form only.
+// A row's bits depend on N only, not on q_rows or on the block it falls in. The variants measured against this form
+// (round 5: 6-wave / 3-chunk workgroups, the attn_step_pl steps, software pipelining, two strips per wave,
+// profiles/r5_lab/attn_stream_*_ab.txt; round 6: ring depths, the step forms and the wave counts,
+// profiles/r6_lab/attn_stream_occupancy_ab.txt, tools/variants/_attn_split.py) are not compiled here.
 constexpr int STREAM_WAVES = 4;
 constexpr int STREAM_CPB = 2;                      // 32-key chunks per group (8 pieces each: 4 per wave per group)
-constexpr int STREAM_RING = 3;                     // groups resident in the ring
+constexpr int STREAM_RING = 2;                     // groups resident in the ring
 constexpr int STREAM_SLOTS = STREAM_CPB * STREAM_RING;
 
-__global__ __launch_bounds__(STREAM_WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void k_attn_stream(
+__global__ __launch_bounds__(STREAM_WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_attn_stream(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, int N, int H, float scale_log2, int q_rows, int QB,
     int BH) {
     constexpr int WAVES = STREAM_WAVES;
@@ -717,18 +682,19 @@ __global__ __launch_bounds__(STREAM_WAVES * 64) __attribute__((amdgpu_waves_per_
     const int st = qb * WAVES + wid;
     const bool act32 = st < SF32 && st * 32 < q_rows;
     const int idle0 = SF32 - (QB - 1) * WAVES;     // first wave of the last block without a 32-query strip
-    const bool act16 = tail >= 1 && tail <= 16 && 32 * SF < q_rows && qb == QB - 1 && wid == (idle0 < WAVES ? idle0 : 0);
+    const bool act16 = tail >= 1 && tail <= 16 && 32 * SF < q_rows && qb == QB - 1 && wid == idle0;   // host: idle0 < WAVES
 
-    // Q fragments by inline-asm loads, unconditionally for both strip kinds (addresses clamped): no branch or merge
-    // between an asm load and the wait that retires it (the rule behind the round-2 / round-4 NaNs, k_attn_bf16_pipe).
-    bf16x8 qf[4], q16[2];
+    // Q fragments by inline-asm loads, one set for both strip kinds with the kind in the address only (k_attn_bf16_pipe's
+    // rule: no branch or merge between an asm load and the wait that retires it). 16-query strip: qf[kk] (kk < 2) =
+    // Q[32 SF + lane % 16][32 kk + 8 (lane / 16) ..] (attn_step16's B operand; qf[2], qf[3] re-read the same bytes).
+    bf16x8 qf[4];
     {
-        const bf16_t* qp = qbase + (int64_t)min(st * 32 + l32, N - 1) * 3 * D + hh * 8;
+        const bf16_t* qp = act16 ? qbase + (int64_t)min(SF * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4)
+                                 : qbase + (int64_t)min(st * 32 + l32, N - 1) * 3 * D + hh * 8;
+        const int step = act16 ? 32 : 16;
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + ks * 16));
-        const bf16_t* qp16 = qbase + (int64_t)min(SF * 32 + (lane & 15), N - 1) * 3 * D + 8 * (lane >> 4);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(q16[kk]) : "v"(qp16 + kk * 32));
+        for (int ks = 0; ks < 4; ++ks)
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + (act16 ? (ks & 1) : ks) * step));
     }
     // group g = chunks [2g, 2g + 2): piece pi = 0..15 of a group is chunk pi / 8, K (pi & 4 == 0) or V, rows 8 (pi & 3) ..
     // + 7 of that chunk (one 1 KiB wave-instruction, lane-linear destination, swizzle on the source address as in
@@ -757,75 +723,86 @@ __global__ __launch_bounds__(STREAM_WAVES * 64) __attribute__((amdgpu_waves_per_
     for (int g = 0; g < g0; ++g) issue_group(g);
     // the Q loads are older than every DMA piece: landed once at most PPW * g0 pieces are outstanding; wait and pin here
     wait_vmcnt(PPW * g0);
-    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(q16[0]), "+v"(q16[1]) :: "memory");
-
-    f32x16 o0 = {}, o1 = {};
-    f32x4 lacc = {};
-    float m = -INFINITY;
-    f32x4 o16[4] = {};
-    float m16 = -INFINITY, l16 = 0.f;
+    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
     const int nfull = N >> 5;                      // chunks without padded keys
-    for (int g = 0; g < NG; ++g) {
-        // this wave's pieces of group g have landed (the groups issued after it stay in flight), then every wave's have
-        const int issued = min(NG, max(STREAM_RING, g + 2));
-        wait_vmcnt(PPW * (issued - g - 1));
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(q16[0]), "+v"(q16[1]) :: "memory");
-        if (g >= 1 && g + 2 < NG) issue_group(g + 2);   // into group g - 1's slots, which every wave has finished
-        const int c_end = min((g + 1) * STREAM_CPB, nfull);
+    // the group loop and the stores of one strip kind; the barrier schedule depends on N only, so every wave of the
+    // workgroup passes the same barriers whatever its kind (or none: act = false keeps the barriers, computes nothing)
+    auto run_strip = [&](auto k16, bool act) {
+        constexpr bool W16 = decltype(k16)::value;
+        f32x16 o0 = {}, o1 = {};
+        f32x4 lacc = {};
+        f32x4 o16[4] = {};
+        float m = -INFINITY, l = 0.f;
+        auto pin_q = [&]() {
+            if constexpr (W16) asm volatile("" : "+v"(qf[0]), "+v"(qf[1]) :: "memory");
+            else asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) :: "memory");
+        };
+        for (int g = 0; g < NG; ++g) {
+            // this wave's pieces of group g have landed (the groups issued after it stay in flight), then every wave's
+            const int issued = min(NG, max(STREAM_RING, g + STREAM_RING - 1));
+            wait_vmcnt(PPW * (issued - g - 1));
+            __builtin_amdgcn_s_barrier();
+            pin_q();
+            // into group g - 1's slots, which every wave has finished
+            if (g >= 1 && g + STREAM_RING - 1 < NG) issue_group(g + STREAM_RING - 1);
+            const int c_end = min((g + 1) * STREAM_CPB, nfull);
 #pragma unroll 1
-        for (int c = g * STREAM_CPB; c < c_end; ++c) {   // the group's chunks without padded keys
-            const int sl = c % STREAM_SLOTS;
+            for (int c = g * STREAM_CPB; c < c_end; ++c) {   // the group's chunks without padded keys
+                const int sl = c % STREAM_SLOTS;
+                const char* Kt = Ks + sl * 4096;
+                const char* Vt = Vs + sl * 4096;
+                if (act) {
+                    if constexpr (W16) attn_step16<false>(Kt, Vt, c * 32, N, lane, qf, scale_log2, m, l, o16);
+                    else attn_step_lf<false>(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
+                }
+            }
+        }
+        if (nfull < NT && act) {   // the chunk with padded keys: the last one, in the last group (its barrier has passed)
+            const int c = nfull, sl = c % STREAM_SLOTS;
             const char* Kt = Ks + sl * 4096;
             const char* Vt = Vs + sl * 4096;
-            if (act32) attn_step_lf<false>(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
-            if (act16) attn_step16<false>(Kt, Vt, c * 32, N, lane, q16, scale_log2, m16, l16, o16);
-        }
-    }
-    if (nfull < NT) {   // the chunk with padded keys: the last one, in the last group (whose barrier has passed)
-        const int c = nfull, sl = c % STREAM_SLOTS;
-        const char* Kt = Ks + sl * 4096;
-        const char* Vt = Vs + sl * 4096;
-        if (act32) {
-            if (N - c * 32 <= 8) attn_step_tail8_lf(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
+            if constexpr (W16) attn_step16<true>(Kt, Vt, c * 32, N, lane, qf, scale_log2, m, l, o16);
+            else if (N - c * 32 <= 8) attn_step_tail8_lf(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
             else attn_step_lf<true>(Kt, Vt, c * 32, N, lane, qf, scale_log2, c == 0, m, lacc, o0, o1);
         }
-        if (act16) attn_step16<true>(Kt, Vt, c * 32, N, lane, q16, scale_log2, m16, l16, o16);
-    }
-    if (act16) {   // the 4 lanes lane % 16 + 16 g share query 32 SF + lane % 16; lane holds dims 16 dt + 4g .. +3
-        const float inv = 1.0f / xor32_sum(xor16_sum(l16));
-        const int qq = SF * 32 + (lane & 15);
-        if (qq < q_rows) {
-            bf16_t* orow = out + (row0 + qq) * D + h * HD + 4 * (lane >> 4);
+        if (!act) return;
+        if constexpr (W16) {   // the 4 lanes lane % 16 + 16 g share query 32 SF + lane % 16; lane: dims 16 dt + 4g .. +3
+            const float inv = 1.0f / xor32_sum(xor16_sum(l));
+            const int qq = SF * 32 + (lane & 15);
+            if (qq < q_rows) {
+                bf16_t* orow = out + (row0 + qq) * D + h * HD + 4 * (lane >> 4);
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-                *reinterpret_cast<uint2*>(orow + 16 * dt) = make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
-                                                                      pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
+                for (int dt = 0; dt < 4; ++dt)
+                    *reinterpret_cast<uint2*>(orow + 16 * dt) = make_uint2(pack_bf2(o16[dt][0] * inv, o16[dt][1] * inv),
+                                                                          pack_bf2(o16[dt][2] * inv, o16[dt][3] * inv));
+            }
+        } else {
+            const float inv = 1.0f / xor32_sum(lacc[0]);
+            uint32_t gx[8], gy[8];   // as k_attn_bf16_pipe: permlane32 pairs -> one 16-B store per 8-dim pair
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const f32x16& o = k < 4 ? o0 : o1;
+                const int b4 = 4 * (k & 3);
+                gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
+                gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
+            }
+            const int q = st * 32 + l32;
+            uint4 ov[4];
+#pragma unroll
+            for (int k = 0; k < 8; k += 2) {
+                const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
+                const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
+                ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+            }
+            if (q < q_rows) {
+                bf16_t* orow = out + (row0 + q) * D + h * HD + 8 * hh;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
+            }
         }
-    }
-    if (!act32) return;
-    const float inv = 1.0f / xor32_sum(lacc[0]);
-    uint32_t gx[8], gy[8];   // as k_attn_bf16_pipe: permlane32 pairs -> one 16-B store per 8-dim pair
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const f32x16& o = k < 4 ? o0 : o1;
-        const int b4 = 4 * (k & 3);
-        gx[k] = pack_bf2(o[b4] * inv, o[b4 + 1] * inv);
-        gy[k] = pack_bf2(o[b4 + 2] * inv, o[b4 + 3] * inv);
-    }
-    const int q = st * 32 + l32;
-    uint4 ov[4];
-#pragma unroll
-    for (int k = 0; k < 8; k += 2) {
-        const auto rx = __builtin_amdgcn_permlane32_swap(gx[k], gx[k + 1], false, false);
-        const auto ry = __builtin_amdgcn_permlane32_swap(gy[k], gy[k + 1], false, false);
-        ov[k >> 1] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
-    }
-    if (q < q_rows) {
-        bf16_t* orow = out + (row0 + q) * D + h * HD + 8 * hh;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(orow + 16 * k) = ov[k];
-    }
+    };
+    if (act16) run_strip(std::true_type{}, true);
+    else run_strip(std::false_type{}, act32);
 }
 
 // CLS-only attention (q_rows == 1: the last encoder block, whose other query rows feed nothing): one wave
@@ -1017,7 +994,9 @@ VPF_API int vpf_attention_bf16(const uint16_t* qkv, uint16_t* out, int64_t B, in
     constexpr int W = STREAM_WAVES;
     const int sf32 = (N >> 5) + ((N & 31) > 16 ? 1 : 0);
     const int need = sf32 < (q_rows + 31) / 32 ? sf32 : (q_rows + 31) / 32;   // 32-query strips holding rows < q_rows
-    const int QB = need > W ? (need + W - 1) / W : 1;
+    const int t32 = N & 31;   // + the 16-query strip, which runs on a wave of its own (k_attn_stream's idle0 < WAVES)
+    const int need16 = need + (t32 >= 1 && t32 <= 16 && 32 * (N >> 5) < q_rows ? 1 : 0);
+    const int QB = need16 > W ? (need16 + W - 1) / W : 1;
     const int64_t blocks = (BH + 7) / 8 * 8 * QB;
     if (blocks > INT32_MAX) return VPF_ERR_ARG;
     hipLaunchKernelGGL(k_attn_stream, dim3((unsigned)blocks), dim3(64 * W), 0,
