@@ -483,7 +483,8 @@ def test_attention_bf16(B, N, H):
 def test_attention_q_rows(dtype, B, N, H):
     """q_rows = 1 (last block: CLS query only) and q_rows = 2 (first strip, partial). bf16 q_rows = 1 runs the
     dedicated fp32-softmax CLS kernel: checked against an fp64 reference; the rows it must not touch stay
-    untouched. q_rows = 2 and fp32 are the same code as the full call: bit-equal."""
+    untouched. q_rows = 2, q_rows = N - 1 (the last query row left out: at N = 577 the 16-query strip's one row) and
+    fp32 are the same code as the full call: bit-equal."""
     torch.manual_seed(3)
     D = 64 * H
     qkv = torch.randn(B, N, 3 * D, device=DEV).to(dtype)
@@ -502,6 +503,10 @@ def test_attention_q_rows(dtype, B, N, H):
     vpf().attention(qkv, H, 2, part2)
     assert torch.equal(part2[:, :2], full[:, :2])
     assert torch.all(part2[:, 2:] == 5.0)
+    part3 = torch.full((B, N, D), 5.0, device=DEV, dtype=dtype)
+    vpf().attention(qkv, H, N - 1, part3)
+    assert torch.equal(part3[:, :N - 1], full[:, :N - 1])
+    assert torch.all(part3[:, N - 1:] == 5.0)
 
 
 @pytest.mark.parametrize("B,N,H", [(3, 197, 12), (5, 197, 6), (2, 256, 12), (4, 1, 6), (64, 50, 12), (2, 577, 16),
@@ -585,15 +590,18 @@ def _attn_ref64(qkv, H):
 
 
 @pytest.mark.parametrize("B,N,H", [(100, 197, 12), (90, 256, 12), (96, 280, 12), (80, 111, 12), (70, 33, 6),
-                                   (4096, 197, 12), (64, 577, 16), (40, 400, 8), (30, 640, 16), (50, 300, 12)])
+                                   (4096, 197, 12), (64, 577, 16), (40, 400, 8), (30, 640, 16), (50, 300, 12),
+                                   (60, 257, 12), (40, 520, 16), (40, 545, 8)])
 def test_attention_bf16_large(B, N, H):
     """B*H >= 4 x CUs; (4096, 197, 12) is the configs[1] launch. N <= 256 runs the key-pipelined kernel (with the
     16-query tail strip when the last strip holds <= 16 real queries: N = 197 / 111 / 33). N > 256 runs the key-streamed
-    kernel (round 5): 4-wave workgroups of 4 x 32-query strips, K / V through a ring of 6 chunk slots (3 groups of 2
-    chunks). N = 577 (configs[3], 64 x 16 units): 5 blocks, the last with 2 strips and the 16-query strip of query 576
-    on a wave of its own; N = 400: 3 blocks, the 16-query strip (16 tail queries) on wave 0 of the last block beside its
-    32-query strip; N = 300: 3 blocks, the 16-query strip on a wave of its own; N = 280: a partial 32-query strip;
-    N = 640: 5 full blocks. Against an fp64 reference on at most 512 particles:
+    kernel: 4-wave workgroups of 4 x 32-query strips, four per CU (round 6), K / V through a ring of 4 chunk slots (2
+    groups of 2 chunks), one strip kind per wave. N = 577 (configs[3], 64 x 16 units): 5 blocks, the last with 2
+    strips and the 16-query strip of query 576 on a wave of its own; N = 400 / 520: 12 / 16 full strips, so the host
+    adds a block whose wave 0 runs the 16-query strip (16 / 8 tail queries) alone; N = 300 / 545: the 16-query strip on
+    a free wave of the last block (12 / 1 tail queries); N = 257: 8 full strips, the added block's 16-query strip holds
+    one query, and the last chunk one real key (the 8-key tail step); N = 280: a partial 32-query strip; N = 640: 5 full blocks. Against an fp64 reference
+    on at most 512 particles:
     every element within bf16 output rounding plus the bf16 probabilities' error, and no non-finite value anywhere
     (the round-2 stale-register NaN). q_rows = 1 (the CLS kernel) likewise."""
     torch.manual_seed(N + H)
