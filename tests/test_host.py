@@ -381,3 +381,36 @@ def test_config_bboxes_validation():
     for bad in ([], [[1, 2, 3]], [[1, 2, 0, 4]], [[1, 2, 3, float("nan")]], "x"):
         with pytest.raises(ValueError):
             C.load_config({"input": {"bboxes": bad}})
+
+
+def test_attention_kernels_fit_their_occupancy_without_spills(tmp_path):
+    """The attention kernels' residency is a design parameter: k_attn_bf16_pipe runs two
+    8-wave workgroups per CU and k_attn_stream (round 6) four 4-wave workgroups, i.e. four waves per SIMD, which holds
+    only at <= 128 VGPRs (+ AGPRs) and, for k_attn_stream, <= 40 KiB of LDS per workgroup. A register spill would also
+    put scratch loads, and the vmcnt waits that retire them, between the K / V DMA pieces and their counted waits.
+    Checked on the compiled gfx950 code: no scratch, the register count and the static LDS size within those bounds."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(ROOT, "vitparticlefiltertracker_amd", "csrc", "attention.hip")
+    out = tmp_path / "attention.s"
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-function", "--cuda-device-only",
+                    "-S", "-o", str(out), src], check=True, capture_output=True)
+    text = out.read_text()
+    seen = set()
+    for m in re.finditer(r"\.amdhsa_kernel (\S+)\n(.*?)\.end_amdhsa_kernel", text, re.S):
+        name, desc = m.group(1), m.group(2)
+        kind = "stream" if "k_attn_stream" in name else "pipe" if "k_attn_bf16_pipe" in name else None
+        if kind is None:
+            continue
+        field = {k: int(v) for k, v in re.findall(r"\.amdhsa_(\w+) (\d+)", desc)}
+        assert field["private_segment_fixed_size"] == 0, (name, "scratch")
+        assert field["next_free_vgpr"] <= 128, (name, field["next_free_vgpr"])
+        if kind == "stream":
+            assert field["group_segment_fixed_size"] <= 40 * 1024, (name, field["group_segment_fixed_size"])
+        body = re.search(r"^" + re.escape(name) + r":(.*?)\.Lfunc_end", text, re.S | re.M).group(1)
+        assert "scratch_" not in body, name
+        seen.add(kind)
+    assert seen == {"stream", "pipe"}, seen
